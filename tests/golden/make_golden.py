@@ -1,0 +1,225 @@
+#!/usr/bin/env python
+"""Generate the golden fixtures in tests/golden/ from the REFERENCE's own Python modules.
+
+Runs only in the survey/build container (needs /root/reference, read-only).  The
+reference is imported with offline stubs (SURVEY.md §8c "working oracle recipe"):
+``cv2`` -> empty module, ``tinycudann`` -> ``oracle.hashgrid.HashGridStub`` (the tcnn
+restatement; hash-grid values are therefore parity-unpinned against real tcnn),
+``nerf_util.sample_dists`` default device -> cpu.  For every case the script
+
+  1. builds ``projects.NeuralLumen.model.Model`` from the reference YAMLs,
+  2. loads seeded synthetic weights (``mli_nerf_amd.synthetic``),
+  3. runs the stage-b forward (train and/or eval), the stage-b losses with the
+     reference's own loss functions, and backward through ``neural_rgb`` only,
+  4. checks ``oracle.render`` against those outputs, and
+  5. saves inputs-that-are-not-regenerable (the stratified uniforms) + outputs as a
+     small ``.pt`` fixture (loaded by the tests with ``weights_only=True``).
+
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+"""
+import os
+import sys
+import types
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = os.environ.get("MLI_REFERENCE", "/root/reference")
+sys.path.insert(0, REPO)
+
+from mli_nerf_amd import synthetic  # noqa: E402
+from mli_nerf_amd.config import load_config  # noqa: E402
+from oracle import hashgrid as o_hash, render as o_render  # noqa: E402
+
+CASES = {
+    # name: (config, R, Nc, Nf, H, log2T, s_var, progress, train, extra overrides)
+    "hotdog_r64_n32_full": ("syn_hotdog_b", 64, 16, 4, 4, 22, 3.0, 0.0, True, {}),
+    "hotdog_r64_n128": ("syn_hotdog_b", 64, 64, 16, 4, 14, 6.0, 0.05, True, {}),
+    "hotdog_r64_n32_eval": ("syn_hotdog_b", 64, 16, 4, 4, 14, 3.0, 1.0, False, {}),
+    "pikachu_r32_n192": ("NRHints_Pikachu_b", 32, 64, 32, 4, 14, 3.0, 0.0, True, {}),
+    "savannah_r64_n32_box": ("rene_savannah_b", 64, 16, 4, 4, 14, 3.0, 0.0, True, {}),
+}
+
+
+def install_stubs():
+    sys.modules["cv2"] = types.ModuleType("cv2")
+    tcnn = types.ModuleType("tinycudann")
+    tcnn.Encoding = o_hash.HashGridStub
+    sys.modules["tinycudann"] = tcnn
+    for name in ("wandb",):
+        sys.modules.setdefault(name, types.ModuleType(name))
+    sys.path.insert(0, REF)
+
+
+def reference_cfg(config, R, Nc, Nf, H, log2T):
+    path = os.path.join(REF, "projects/NeuralLumen/configs/%s.yaml" % config)
+    over = {"model": {"render": {"rand_rays": R, "num_samples": {"coarse": Nc, "fine": Nf},
+                                 "num_sample_hierarchy": H},
+                      "object": {"sdf": {"encoding": {"hashgrid": {"dict_size": log2T}}}}}}
+    return load_config(path, root=REF, overrides=over)
+
+
+def path_cfg(cfg, Nc, Nf, H, log2T):
+    box = getattr(cfg.data, "bounding_type", "unit_sphere") == "box"
+    return o_render.PathCfg(n_coarse=Nc, n_fine=Nf, n_hier=H, log2T=log2T,
+                            white_bg=bool(cfg.model.background.white),
+                            bounding="box" if box else "sphere",
+                            aabb=tuple(cfg.data.bounding_box_aabb) if box else (-1, -1, -1, 1, 1, 1))
+
+
+def load_weights(model, sd):
+    tgt = model.state_dict()
+    missing = [k for k in tgt if k not in sd]
+    assert not missing, missing
+    with torch.no_grad():
+        for k, v in sd.items():
+            if k == "neural_sdf.tcnn_encoding.params":
+                model.neural_sdf.tcnn_encoding.params = v.clone()
+            else:
+                tgt[k].copy_(v)
+
+
+def ref_losses(out, data, cfg):
+    from projects.NeuralLumen.utils.utils import intrinsic_loss, regularize_re_loss
+    from projects.neuralangelo.utils.misc import eikonal_loss, curvature_loss
+    p = cfg.trainer.para_intrinsic_loss
+    q = cfg.trainer.para_regularize_re_loss
+    losses = dict(
+        render=torch.nn.L1Loss()(out["rgb"], data["image_sampled"]) * 3,
+        eikonal=eikonal_loss(out["gradients"], outside=out["outside"]),
+        curvature=curvature_loss(out["hessians"], outside=out["outside"]),
+        intrinsic=intrinsic_loss(out["o_r"], out["o_s"], data["pseudo_ref_sampled"],
+                                 data["pseudo_sha_sampled"], data["pseudo_visibility_certainty_sampled"],
+                                 weight_map_range_shading=tuple(p["weight_map_range_shading"]),
+                                 weight_map_range_visibility=tuple(p["weight_map_range_visibility"]),
+                                 factor_ref=p["factor_ref"], factor_sha=p["factor_sha"]),
+        regularize_re=regularize_re_loss(out["o_re"], factor_negative=q["factor_negative"],
+                                         factor_positive=q["factor_positive"],
+                                         exponent_positive=q["exponent_positive"]),
+    )
+    weights = {k: v for k, v in cfg.trainer.loss_weight.items() if v}
+    total = sum(losses[k] * weights[k] for k in weights if k in losses)
+    return total, losses
+
+
+def grad_digest(named_grads):
+    """Full grads of biases/weight_g + a fixed strided subset of every weight_v."""
+    out = {}
+    for k, g in named_grads.items():
+        if k.endswith("weight_v"):
+            out[k + ":strided"] = g.flatten()[::97].clone()
+            out[k + ":sum"] = g.double().sum().float()
+        else:
+            out[k] = g.clone()
+    return out
+
+
+def run_case(name, spec):
+    from projects.nerf.utils import nerf_util
+    from projects.NeuralLumen.model import Model
+    config, R, Nc, Nf, H, log2T, s_var, progress, train, _ = spec
+    nerf_util.sample_dists.__defaults__ = ("cpu",)
+    cfg = reference_cfg(config, R, Nc, Nf, H, log2T)
+    H_img, W_img = cfg.data.train.image_size
+    model = Model(cfg.model, cfg.data)
+    sd = synthetic.make_state_dict(log2T=log2T, seed=0, s_var=s_var)
+    load_weights(model, sd)
+    model.neural_sdf.set_normal_epsilon()
+    model.progress = progress
+    if hasattr(model, "bounding_box_aabb"):
+        model.bounding_box_aabb = model.bounding_box_aabb.float()
+    data = synthetic.make_batch(R, H=H_img, W=W_img, frame=3)
+    for p_name, p in model.named_parameters():
+        p.requires_grad_(p_name.startswith("neural_rgb"))
+    torch.manual_seed(1234)
+    u = torch.rand(1, R, Nc)  # what sample_dists draws first after this seed
+    fix = dict(R=R, Nc=Nc, Nf=Nf, H=H, log2T=log2T, s_var=s_var, progress=progress, train=train,
+               config=config, H_img=H_img, W_img=W_img)
+    pcfg = path_cfg(cfg, Nc, Nf, H, log2T)
+    if train:
+        model.train()
+        torch.manual_seed(1234)
+        out = model(data)
+        total, losses = ref_losses(out, data, cfg)
+        total.backward()
+        grads = {k: p.grad for k, p in model.named_parameters() if p.grad is not None}
+        fix["u"] = u
+        for k in ("rgb", "o_r", "o_s", "o_re", "dists", "weights", "gradients", "hessians", "outside"):
+            fix["out." + k] = out[k].detach().clone()
+        fix["loss.total"] = total.detach()
+        for k, v in losses.items():
+            fix["loss." + k] = v.detach()
+        fix.update({"grad." + k: v for k, v in grad_digest(grads).items()})
+        # oracle check
+        sd_o = {k: v.clone().requires_grad_(k.startswith("neural_rgb")) for k, v in sd.items()}
+        o_out = o_render.forward(sd_o, pcfg, data, u=u, training=True, progress=progress, width=W_img,
+                                 height=H_img)
+        o_total, o_losses, _ = o_render.stage_b_losses(o_out, data, pcfg)
+        o_total.backward()
+        check(name, fix, o_out, o_losses, o_total, {k: sd_o[k].grad for k in grads})
+    else:
+        model.eval()
+        from projects.nerf.utils import camera
+        import torch.nn.functional as F
+        from projects.NeuralLumen.utils.utils import get_center
+        with torch.no_grad():
+            center, ray = camera.get_center_and_ray(data["pose"], data["intr"], (H_img, W_img))
+            center = nerf_util.slice_by_ray_idx(center, data["ray_idx"])
+            ray = nerf_util.slice_by_ray_idx(ray, data["ray_idx"])
+            pts_light = nerf_util.slice_by_ray_idx(get_center(data["pose_light"], (H_img, W_img)),
+                                                   data["ray_idx"])
+            out = model.render_rays_lumen(center, F.normalize(ray, dim=-1), pts_light, stratified=False)
+            out["depth"] = (out["dists"] * out["weights"]).sum(2) / ray.norm(dim=-1, keepdim=True)
+        for k in ("rgb", "o_r", "o_s", "o_re", "dists", "weights", "gradients", "opacity",
+                  "gradient", "depth", "outside"):
+            fix["out." + k] = out[k].detach().clone()
+        with torch.no_grad():
+            o_out = o_render.forward(sd, pcfg, data, u=None, training=False, progress=progress,
+                                     width=W_img, height=H_img)
+        check(name, fix, o_out, None, None, None)
+    path = os.path.join(HERE, name + ".pt")
+    torch.save(fix, path)
+    print("wrote %s (%.1f KB)" % (path, os.path.getsize(path) / 1024))
+
+
+def check(name, fix, o_out, o_losses, o_total, o_grads):
+    worst = 0.0
+    for k, v in fix.items():
+        if not k.startswith("out.") or k[4:] in ("depth",):
+            continue
+        o = o_out[k[4:]]
+        if v.dtype == torch.bool:
+            assert torch.equal(v, o), (name, k)
+            continue
+        err = (v - o.detach()).abs().max().item()
+        tol = 1e-4 + 1e-4 * v.abs().max().item()
+        if k[4:] == "hessians":
+            tol = 1e-2 * max(1.0, v.abs().max().item())
+        worst = max(worst, err / tol)
+        assert err <= tol, (name, k, err, tol)
+    if o_losses is not None:
+        for k, v in o_losses.items():
+            r = fix["loss." + k].item()
+            assert abs(r - v.item()) <= 1e-4 * max(1.0, abs(r)), (name, k, r, v.item())
+        for k, g in o_grads.items():
+            ref = fix.get("grad." + k)
+            if ref is None:
+                ref = fix["grad." + k + ":strided"]
+                g = g.flatten()[::97]
+            err = (ref - g).abs().max().item()
+            assert err <= 1e-5 + 1e-3 * ref.abs().max().item(), (name, k, err)
+    print("%s: oracle matches reference (worst err/tol %.3f)" % (name, worst))
+
+
+def main():
+    install_stubs()
+    only = sys.argv[1:]
+    for name, spec in CASES.items():
+        if only and name not in only:
+            continue
+        run_case(name, spec)
+
+
+if __name__ == "__main__":
+    main()
