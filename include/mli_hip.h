@@ -1,0 +1,292 @@
+/*
+ * mli_hip.h -- C ABI of libmli_hip.so, the MI355X (gfx950) kernels of the MLI-NeRF
+ * stage-b volume-rendering hot path.
+ *
+ * Every entry point has the shape   int mli_<op>(const mli_<op>_args* a, hipStream_t s)
+ * and returns a hipError_t value (0 = success).  No exceptions cross the ABI.
+ *
+ * Ownership: the caller (PyTorch on the Python side) allocates every buffer; the library
+ * never allocates or frees device memory and never synchronises.  Entry points are
+ * re-entrant (no global mutable state) and enqueue on the given stream only, so they
+ * can be captured into a hipGraph.
+ *
+ * Layout conventions (R rays, N samples per ray, S = R*N, B = 1 image per rank as in
+ * every reference config, syn_hotdog_b.yaml:38):
+ *   [R,3]      ray-major xyz
+ *   [N][R]     sample-major per-sample scalars: element (ray r, sample k) at k*R + r
+ *   [N][R][c]  sample-major per-sample vectors
+ *   "tile order" for the MLP kernels: m = r*N + k, tiles of 32 consecutive m (a wave),
+ *   workgroups of 256 (8 waves).  S must be a multiple of 32.
+ *   frag image: fp16 activations of a 32-sample tile in MFMA B-operand register order,
+ *   [S/32][ksteps][64 lanes][8 halves] (16 B per lane per k-step, 1 KiB per wave load).
+ *   feature-major: [features][S] fp16 rows (S contiguous), in tile order m.
+ *
+ * Reference interface each entry point replaces is cited per function
+ * (paths relative to the liulisixin/MLI-NeRF checkout).
+ */
+#ifndef MLI_HIP_H
+#define MLI_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* mli_stream_t; /* == hipStream_t */
+
+#define MLI_ABI_VERSION 1
+#define MLI_HIDDEN 256
+#define MLI_LEVELS 16
+#define MLI_LEVEL_FEAT 8
+#define MLI_HEAD_K0 304 /* packed head layer-0 input rows: feat 256 | p,n 6 | pad 10 | light 16 | view 16 */
+
+/* Per-level hash-grid geometry, passed BY VALUE (host fills it from layout/level_table). */
+typedef struct {
+  float scale[MLI_LEVELS];
+  uint32_t res[MLI_LEVELS];
+  uint32_t size[MLI_LEVELS];
+  uint32_t offset[MLI_LEVELS];
+  uint64_t modmagic[MLI_LEVELS]; /* Lemire fastmod M = 2^64 / size + 1 (dense levels)  */
+} mli_grid_levels;
+
+int mli_abi_version(void);
+const char* mli_error_string(int code);
+
+/* ---------------------------------------------------------------- rays + bounds
+ * Replaces camera.get_center_and_ray + slice_by_ray_idx (projects/nerf/utils/camera.py:283-311,
+ * projects/nerf/utils/nerf_util.py:127-131), get_center (NeuralLumen/utils/utils.py:61-79),
+ * F.normalize (NeuralLumen/model.py:125) and get_dist_bounds (neuralangelo/model.py:420-430,
+ * nerf_util.py:199-205, NeuralLumen/utils/utils.py:86-123).  Only the R sampled rays are built. */
+typedef struct {
+  const float* intr_inv;  /* [3,3] inverse intrinsics (host: intr.inverse())            */
+  const float* c2w;       /* [3,4] Pose.invert(pose)                                      */
+  const float* c2w_light; /* [3,4] Pose.invert(pose_light)                                */
+  const int64_t* ray_idx; /* [R] flat pixel index y*W + x (NULL: ray r = pixel first+r)   */
+  int64_t first_pixel;    /* used when ray_idx == NULL (full-image chunks)                */
+  int R, W;
+  int bounding;           /* 0: unit sphere, 1: AABB                                      */
+  float aabb[6];
+  float* center;          /* [R,3] */
+  float* ray_unit;        /* [R,3] */
+  float* ray_norm;        /* [R]   ||ray|| (depth = dist / ||ray||, NeuralLumen/model.py:103) */
+  float* pts_light;       /* [R,3] */
+  float* near_;           /* [R]   */
+  float* far_;            /* [R]   */
+  uint8_t* outside;       /* [R]   */
+} mli_rays_args;
+int mli_rays(const mli_rays_args* a, mli_stream_t s);
+
+/* ---------------------------------------------------------------- hash-grid encode
+ * Replaces tcnn.Encoding(HashGrid) forward (neuralangelo/utils/modules.py:42-50,83-86);
+ * semantics restated in oracle/hashgrid.py.  Standalone op (the fused SDF kernels below
+ * call the same device code). */
+typedef struct {
+  const float* x01;       /* [n,3] in [0,1] = (p + 2) / 4                                  */
+  const uint16_t* table;  /* fp16 shadow of neural_sdf.tcnn_encoding.params [entries*8]    */
+  mli_grid_levels levels;
+  int n;
+  float* out;             /* [n,128] fp32, level-major                                     */
+} mli_hashgrid_args;
+int mli_hashgrid_fwd(const mli_hashgrid_args* a, mli_stream_t s);
+
+/* ---------------------------------------------------------------- neural SDF
+ * Replaces NeuralSDF.forward/sdf (neuralangelo/utils/modules.py:68-95), MLPforNeuralSDF
+ * layer 0 + sdf head (neuralangelo/utils/mlp.py:55-69) and, in FIELD mode, the 4-tap
+ * numerical gradient/hessian (modules.py:157-175) + outside overwrite (NeuralLumen/model.py:343).
+ * Points are p = center_r + ray_unit_r * dists[k][r] with sample m = r*n_per_ray + k.
+ * Weights: `wsdf` from mli_pack (layout MLI_SDF_PACK_*). */
+#define MLI_SDF_MODE_SDF 0   /* sdf only                                                   */
+#define MLI_SDF_MODE_FIELD 1 /* sdf (+outside), grad, hess, h0 frag image                  */
+typedef struct {
+  int mode;
+  int R, n_per_ray;
+  const float* center;
+  const float* ray_unit;
+  const float* dists;     /* [n_per_ray][R] */
+  const uint8_t* outside; /* [R] (FIELD) */
+  const uint16_t* table;  /* fp16 hash table */
+  mli_grid_levels levels;
+  const void* wsdf;       /* packed SDF layer-0 block (mli_pack) */
+  float eps;              /* tap epsilon = normal_eps / sqrt(3) (fp32)                    */
+  float grad_den;         /* fp32(4 * eps)      (modules.py:167)                           */
+  float hess_den;         /* fp32(eps ** 2)     (modules.py:172)                           */
+  float outside_val;      /* 1000                                                          */
+  int with_hessian;
+  float* sdf;             /* [n_per_ray][R] */
+  float* grad;            /* [n_per_ray][R][3] (FIELD) */
+  float* hess;            /* [n_per_ray][R][3] (FIELD, with_hessian) */
+  uint16_t* h0;           /* frag image [S/32][16][64][8] (FIELD) */
+} mli_sdf_args;
+int mli_sdf(const mli_sdf_args* a, mli_stream_t s);
+
+/* ---------------------------------------------------------------- sampling
+ * Replaces nerf_util.sample_dists (nerf_util.py:20-38), sample_dists_hierarchical
+ * (neuralangelo/model.py:467-484), sample_dists_from_pdf (nerf_util.py:41-68) and the
+ * cat + sort + gather of sample_dists_all (neuralangelo/model.py:449-465). */
+typedef struct {
+  const float* near_; const float* far_;
+  const float* u;         /* [R][Nc] stratified uniforms, NULL -> 0.5 (eval) */
+  int R, Nc;
+  float* dists;           /* [Nc][R] */
+} mli_sample_coarse_args;
+int mli_sample_coarse(const mli_sample_coarse_args* a, mli_stream_t s);
+
+typedef struct {
+  int R;
+  const float* dists_a; const float* sdf_a; int Na;  /* sorted list so far [Na][R]        */
+  const float* dists_b; const float* sdf_b; int Nb;  /* previous fine samples (Nb may be 0) */
+  float* dists_out; float* sdf_out;                  /* merged [Na+Nb][R] (sdf_out may be NULL) */
+  int Nf;                 /* fine samples to draw (0: merge only)                          */
+  float inv_s;            /* 64 * 2^h                                                      */
+  const float* u_fine;    /* [Nf] midpoint quantiles (torch.linspace semantics, host)       */
+  float* fine_out;        /* [Nf][R] */
+} mli_sample_fine_args;
+int mli_sample_fine(const mli_sample_fine_args* a, mli_stream_t s);
+
+/* ---------------------------------------------------------------- light-conditioned heads
+ * Replaces MLPforNeuralSDF layer 1 (feat, mlp.py:61-64) and LumenRGB.forward mode
+ * 'rgb_r_s' (NeuralLumen/utils/modules.py:106-109,148-163): SH16 of the view direction and
+ * of the raw light position (spherical_harmonics.py:47-84), three weight-normed
+ * 5-layer ReLU MLPs (nerf_util.py:158-196) and sigmoid outputs, on fp16 MFMA with fp32
+ * accumulation.  Training mode also writes what mli_rgb_bwd / mli_wgrad need. */
+typedef struct {
+  int R, N;
+  const float* center; const float* ray_unit; const float* pts_light;
+  const float* dists;     /* [N][R] */
+  const float* grad;      /* [N][R][3] normals = normalize(grad)                           */
+  const uint16_t* h0;     /* frag image from mli_sdf FIELD                                 */
+  const void* wfwd;       /* packed forward weight chunks (mli_pack)                       */
+  float* y;               /* [N][R][8] rgb(3) o_r(3) o_s(1) pad                            */
+  uint16_t* feat_frag;    /* scratch frag image [S/32][16][64][8]                          */
+  /* training outputs (NULL in inference) */
+  uint16_t* x0T;          /* [MLI_HEAD_K0][S] feature-major head input                      */
+  uint16_t* xT;           /* [3 heads][4 layers][256][S] feature-major X1..X4               */
+  uint32_t* masks;        /* [3][4][S/32][64][4] ReLU bit masks of X1..X4                   */
+} mli_rgb_fwd_args;
+int mli_rgb_fwd(const mli_rgb_fwd_args* a, mli_stream_t s);
+
+/* ---------------------------------------------------------------- compositing
+ * Replaces compute_neus_alphas/_get_iter_cos (neuralangelo/model.py:492-515),
+ * alpha_compositing_weights + composite (nerf/utils/render.py:87-112) and the intrinsic
+ * assembly of render_rays_lumen (NeuralLumen/model.py:266-305) incl. white background
+ * and o_re; eval adds opacity, gradient and depth (NeuralLumen/model.py:101-104). */
+typedef struct {
+  int R, N;
+  const float* dists; const float* far_; const float* ray_unit; const float* ray_norm;
+  const float* sdf; const float* grad; const float* y;
+  const float* s_var;     /* device scalar: inv_s = exp(s_var)                             */
+  float anneal;           /* min(progress / anneal_end, 1)                                 */
+  int white_bg;
+  float* weights;         /* [N][R] */
+  float* rgb; float* o_r; float* o_s; float* o_re;   /* [R,3],[R,3],[R],[R,3]             */
+  float* opacity; float* gradient; float* depth;     /* [R],[R,3],[R] (NULL to skip)      */
+} mli_composite_args;
+int mli_composite_fwd(const mli_composite_args* a, mli_stream_t s);
+
+/* Backward of the composite w.r.t. the head outputs: per-sample dZ4 = dy*y*(1-y)*scale. */
+typedef struct {
+  int R, N;
+  const float* weights; const float* y;
+  const float* o_r; const float* o_s;                 /* composited [R,3], [R] */
+  const float* d_rgb; const float* d_o_r; const float* d_o_s; const float* d_o_re;
+  float grad_scale;       /* power of two, undone in mli_grad_assemble                     */
+  float* dz4;             /* [N][R][8] scaled pre-sigmoid grads: rgb(3) r(3) s(1) pad       */
+} mli_composite_bwd_args;
+int mli_composite_bwd(const mli_composite_bwd_args* a, mli_stream_t s);
+
+/* ---------------------------------------------------------------- heads backward
+ * dX chain of the three heads (ReLU masks from the forward), writing feature-major
+ * dZ_l for the weight gradients.  Replaces autograd through MLPwithSkipConnection. */
+typedef struct {
+  int R, N;
+  const float* dz4;       /* [N][R][8] */
+  const void* wbwd;       /* packed transposed weight chunks (mli_pack)                     */
+  const uint32_t* masks;  /* from mli_rgb_fwd */
+  uint16_t* dzT;          /* [3 heads][4 layers][256][S] feature-major dZ0..dZ3 (scaled)    */
+  uint16_t* dz4T;         /* [3 heads][4][S] feature-major dZ4 rows (scaled)                */
+} mli_rgb_bwd_args;
+int mli_rgb_bwd(const mli_rgb_bwd_args* a, mli_stream_t s);
+
+/* Weight/bias gradients dW_l = dZ_l^T X_l, db_l = sum dZ_l (split-K MFMA GEMM, fp32 atomics
+ * into dw/db which the caller zeroes).  Jobs are described in mli_nerf_amd/layout.py. */
+typedef struct {
+  const uint16_t* a_rows; /* dZ^T rows [M][S] */
+  const uint16_t* b_rows; /* X^T  rows [K][S] */
+  int M, K;               /* logical rows of A and B */
+  float* dw;              /* [M][K] fp32 (row stride K) */
+  float* db;              /* [M] fp32 or NULL */
+} mli_wgrad_job;
+typedef struct {
+  int S;
+  int n_jobs;
+  const mli_wgrad_job* jobs; /* HOST array (copied into the kernel arguments) */
+  int k_split;            /* samples per workgroup (multiple of 64)                          */
+} mli_wgrad_args;
+int mli_wgrad(const mli_wgrad_args* a, mli_stream_t s);
+
+/* ---------------------------------------------------------------- parameters
+ * Weight-norm W = g * v / ||v||_row (torch.nn.utils.weight_norm dim=0) folded once per
+ * step and packed into the fp16 MFMA chunk images the kernels stream; layer descriptors
+ * built on the host (mli_nerf_amd/layout.py). */
+typedef struct {
+  const float* v; const float* g; const float* bias; /* reference tensors (fp32)         */
+  int n_out, k_ref;       /* v is [n_out][k_ref]                                          */
+  int transpose;          /* 0: pack W (rows n_out), 1: pack W^T (rows k_ref)              */
+  int n_tiles, k_steps;   /* packed geometry: rows n_tiles*32, k_steps*16                  */
+  const int16_t* kmap;    /* [k_steps*16] packed k -> source index (-1: zero)              */
+  const uint8_t* kmode;   /* [k_steps] 0: NAT, 1: ACC ordering                             */
+  int64_t dst_offset;     /* byte offset of the first chunk in dst                         */
+  int chunk_stride;       /* bytes per chunk (k_steps*1024 + 128)                          */
+} mli_pack_layer;
+typedef struct {
+  int n_layers;
+  const mli_pack_layer* layers; /* DEVICE array of descriptors */
+  uint8_t* dst;
+} mli_pack_args;
+int mli_pack(const mli_pack_args* a, mli_stream_t s);
+
+/* SDF layer-0 block: fp16 fragments of W0[:, 3:] + fp32 row constants (see layout.py). */
+typedef struct {
+  const float* v0; const float* g0; const float* b0;  /* linears.0 [256,131]              */
+  const float* w_sdf; const float* b_sdf;             /* linear_sdf [1,256], [1]          */
+  uint8_t* dst;           /* MLI_SDF_PACK_BYTES */
+} mli_pack_sdf_args;
+#define MLI_SDF_PACK_BYTES (65536 + 5 * 1024 + 16)
+int mli_pack_sdf(const mli_pack_sdf_args* a, mli_stream_t s);
+
+/* dW (packed-k order) -> reference-layout grads of weight_v / weight_g / bias through the
+ * weight-norm backward, scaled by 1/grad_scale, written into the flat grad buffer. */
+typedef struct {
+  const float* dw; const float* db;    /* [n_out][k_pack], [n_out] */
+  const float* v; const float* g;
+  int n_out, k_ref, k_pack;
+  const int16_t* kinv;    /* [k_ref] reference column -> packed k                         */
+  float* grad_v; float* grad_g; float* grad_b;
+  const float* extra_db;  /* NULL */
+} mli_assemble_layer;
+typedef struct {
+  int n_layers;
+  const mli_assemble_layer* layers; /* DEVICE array */
+  float inv_scale;
+} mli_assemble_args;
+int mli_grad_assemble(const mli_assemble_args* a, mli_stream_t s);
+
+/* AdamW over one flat fp32 parameter buffer (torch.optim.AdamW semantics,
+ * imaginaire/trainers/utils/get_trainer.py:106-150, base.yaml:117-127). */
+typedef struct {
+  float* p; const float* g; float* m; float* v;
+  int64_t n;
+  float lr, beta1, beta2, eps, weight_decay;
+  int step;               /* 1-based step after increment */
+} mli_adamw_args;
+int mli_adamw(const mli_adamw_args* a, mli_stream_t s);
+
+/* fp32 -> fp16 copy (hash-table shadow). */
+typedef struct { const float* src; uint16_t* dst; int64_t n; } mli_cast_args;
+int mli_cast_f16(const mli_cast_args* a, mli_stream_t s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MLI_HIP_H */

@@ -1,0 +1,155 @@
+"""ctypes binding of libmli_hip.so (include/mli_hip.h).  Fails loudly if the library is
+missing -- there is no CPU fallback on the product path."""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmli_hip.so")
+
+P = C.c_void_p
+I32 = C.c_int
+I64 = C.c_int64
+F32 = C.c_float
+
+
+class GridLevels(C.Structure):
+    _fields_ = [("scale", F32 * 16), ("res", C.c_uint32 * 16), ("size", C.c_uint32 * 16),
+                ("offset", C.c_uint32 * 16), ("modmagic", C.c_uint64 * 16)]
+
+
+class RaysArgs(C.Structure):
+    _fields_ = [("intr_inv", P), ("c2w", P), ("c2w_light", P), ("ray_idx", P), ("first_pixel", I64),
+                ("R", I32), ("W", I32), ("bounding", I32), ("aabb", F32 * 6),
+                ("center", P), ("ray_unit", P), ("ray_norm", P), ("pts_light", P),
+                ("near_", P), ("far_", P), ("outside", P)]
+
+
+class HashgridArgs(C.Structure):
+    _fields_ = [("x01", P), ("table", P), ("levels", GridLevels), ("n", I32), ("out", P)]
+
+
+class SdfArgs(C.Structure):
+    _fields_ = [("mode", I32), ("R", I32), ("n_per_ray", I32), ("center", P), ("ray_unit", P),
+                ("dists", P), ("outside", P), ("table", P), ("levels", GridLevels), ("wsdf", P),
+                ("eps", F32), ("grad_den", F32), ("hess_den", F32), ("outside_val", F32),
+                ("with_hessian", I32), ("sdf", P), ("grad", P), ("hess", P), ("h0", P)]
+
+
+class SampleCoarseArgs(C.Structure):
+    _fields_ = [("near_", P), ("far_", P), ("u", P), ("R", I32), ("Nc", I32), ("dists", P)]
+
+
+class SampleFineArgs(C.Structure):
+    _fields_ = [("R", I32), ("dists_a", P), ("sdf_a", P), ("Na", I32), ("dists_b", P), ("sdf_b", P),
+                ("Nb", I32), ("dists_out", P), ("sdf_out", P), ("Nf", I32), ("inv_s", F32),
+                ("u_fine", P), ("fine_out", P)]
+
+
+class RgbFwdArgs(C.Structure):
+    _fields_ = [("R", I32), ("N", I32), ("center", P), ("ray_unit", P), ("pts_light", P),
+                ("dists", P), ("grad", P), ("h0", P), ("wfwd", P), ("y", P), ("feat_frag", P),
+                ("x0T", P), ("xT", P), ("masks", P)]
+
+
+class CompositeArgs(C.Structure):
+    _fields_ = [("R", I32), ("N", I32), ("dists", P), ("far_", P), ("ray_unit", P), ("ray_norm", P),
+                ("sdf", P), ("grad", P), ("y", P), ("s_var", P), ("anneal", F32), ("white_bg", I32),
+                ("weights", P), ("rgb", P), ("o_r", P), ("o_s", P), ("o_re", P), ("opacity", P),
+                ("gradient", P), ("depth", P)]
+
+
+class CompositeBwdArgs(C.Structure):
+    _fields_ = [("R", I32), ("N", I32), ("weights", P), ("y", P), ("o_r", P), ("o_s", P),
+                ("d_rgb", P), ("d_o_r", P), ("d_o_s", P), ("d_o_re", P), ("grad_scale", F32),
+                ("dz4", P)]
+
+
+class RgbBwdArgs(C.Structure):
+    _fields_ = [("R", I32), ("N", I32), ("dz4", P), ("wbwd", P), ("masks", P), ("dzT", P),
+                ("dz4T", P)]
+
+
+class WgradJob(C.Structure):
+    _fields_ = [("a_rows", P), ("b_rows", P), ("M", I32), ("K", I32), ("dw", P), ("db", P)]
+
+
+class WgradArgs(C.Structure):
+    _fields_ = [("S", I32), ("n_jobs", I32), ("jobs", P), ("k_split", I32)]
+
+
+class PackLayer(C.Structure):
+    _fields_ = [("v", P), ("g", P), ("bias", P), ("n_out", I32), ("k_ref", I32), ("transpose", I32),
+                ("n_tiles", I32), ("k_steps", I32), ("kmap", P), ("kmode", P), ("dst_offset", I64),
+                ("chunk_stride", I32)]
+
+
+class PackArgs(C.Structure):
+    _fields_ = [("n_layers", I32), ("layers", P), ("dst", P)]
+
+
+class PackSdfArgs(C.Structure):
+    _fields_ = [("v0", P), ("g0", P), ("b0", P), ("w_sdf", P), ("b_sdf", P), ("dst", P)]
+
+
+class AssembleLayer(C.Structure):
+    _fields_ = [("dw", P), ("db", P), ("v", P), ("g", P), ("n_out", I32), ("k_ref", I32),
+                ("k_pack", I32), ("kinv", P), ("grad_v", P), ("grad_g", P), ("grad_b", P),
+                ("extra_db", P)]
+
+
+class AssembleArgs(C.Structure):
+    _fields_ = [("n_layers", I32), ("layers", P), ("inv_scale", F32)]
+
+
+class AdamwArgs(C.Structure):
+    _fields_ = [("p", P), ("g", P), ("m", P), ("v", P), ("n", I64), ("lr", F32), ("beta1", F32),
+                ("beta2", F32), ("eps", F32), ("weight_decay", F32), ("step", I32)]
+
+
+class CastArgs(C.Structure):
+    _fields_ = [("src", P), ("dst", P), ("n", I64)]
+
+
+ENTRY_POINTS = {
+    "mli_rays": RaysArgs, "mli_hashgrid_fwd": HashgridArgs, "mli_sdf": SdfArgs,
+    "mli_sample_coarse": SampleCoarseArgs, "mli_sample_fine": SampleFineArgs,
+    "mli_rgb_fwd": RgbFwdArgs, "mli_composite_fwd": CompositeArgs,
+    "mli_composite_bwd": CompositeBwdArgs, "mli_rgb_bwd": RgbBwdArgs, "mli_wgrad": WgradArgs,
+    "mli_pack": PackArgs, "mli_pack_sdf": PackSdfArgs, "mli_grad_assemble": AssembleArgs,
+    "mli_adamw": AdamwArgs, "mli_cast_f16": CastArgs,
+}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("libmli_hip.so is not built (%s); run mli_nerf_amd.build.build() -- "
+                              "there is no CPU fallback for the hot path" % LIB_PATH)
+        _lib = C.CDLL(LIB_PATH)
+        for name, st in ENTRY_POINTS.items():
+            fn = getattr(_lib, name)
+            fn.argtypes = [C.POINTER(st), P]
+            fn.restype = I32
+        _lib.mli_abi_version.restype = I32
+        _lib.mli_error_string.restype = C.c_char_p
+        _lib.mli_error_string.argtypes = [I32]
+        if _lib.mli_abi_version() != 1:
+            raise ImportError("libmli_hip.so ABI mismatch")
+    return _lib
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+def call(name, args, stream=None):
+    import torch
+    if stream is None:
+        stream = torch.cuda.current_stream().cuda_stream
+    rc = getattr(lib(), name)(C.byref(args), stream)
+    if rc != 0:
+        raise RuntimeError("%s failed: %s (%d)" % (name, lib().mli_error_string(rc).decode(), rc))

@@ -1,0 +1,49 @@
+"""Build libmli_hip.so (gfx950) in-tree with hipcc.  ``python -m mli_nerf_amd.build``."""
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "libmli_hip.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+SOURCES = ["rays.hip", "sdf.hip", "mlp.hip", "wgrad.hip", "params.hip"]
+FLAGS = ["-O3", "--offload-arch=gfx950", "-fPIC", "-std=c++17", "-ffp-contract=off",
+         "-I", os.path.join(REPO, "include"), "-I", CSRC]
+
+
+def _compile(src, extra):
+    obj = os.path.join(CSRC, "build", os.path.splitext(src)[0] + ".o")
+    os.makedirs(os.path.dirname(obj), exist_ok=True)
+    cmd = [HIPCC] + FLAGS + list(extra) + ["-c", os.path.join(CSRC, src), "-o", obj]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError("hipcc failed for %s:\n%s" % (src, res.stderr))
+    return obj, res.stderr
+
+
+def build(verbose=False, extra=()):
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + [
+        os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + [
+        os.path.join(REPO, "include", "mli_hip.h")]
+    if os.path.exists(OUT) and not extra and all(os.path.getmtime(d) <= os.path.getmtime(OUT) for d in deps):
+        return OUT
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
+        results = list(ex.map(lambda s: _compile(s, extra), SOURCES))
+    if verbose:
+        for _, log in results:
+            if log:
+                print(log)
+    objs = [o for o, _ in results]
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT] + objs
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError("link failed:\n" + res.stderr)
+    return OUT
+
+
+if __name__ == "__main__":
+    extra = sys.argv[1:]
+    print(build(verbose=True, extra=extra))

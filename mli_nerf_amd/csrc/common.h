@@ -1,0 +1,88 @@
+// Shared device helpers for the gfx950 kernels of libmli_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mli_hip.h"
+
+typedef _Float16 f16;
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#define MLI_FI __device__ __forceinline__
+#define MLI_LAMBDA_FI __attribute__((always_inline))
+
+// D = A(32x16) * B(16x32) + C on one wave (gfx950 v_mfma_f32_32x32x16_f16).
+// Lane l (r = l & 31, h = l >> 5) holds A[r][k(h,j)] and B[k(h,j)][r] in element j;
+// D register i of lane l is element (row = acc_row(i, h), col = r).
+MLI_FI f32x16 mfma32(half8 a, half8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+// Row of the 32x32 D tile held by accumulator register i in lane half h.
+MLI_FI int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+// Packed-k index of element j, lane half h, k-step q:
+//   NAT: the natural B-operand order; ACC: the order an accumulator tile has when its
+//   registers 8s..8s+7 are reused as the B fragment of k-step 2t+s (guide §3).
+MLI_FI int k_nat(int q, int h, int j) { return 16 * q + 8 * h + j; }
+MLI_FI int k_acc(int q, int h, int j) { return 16 * q + 8 * (j >> 2) + 4 * h + (j & 3); }
+
+// Convert accumulator registers [8s, 8s+8) to the fp16 B fragment of k-step 2t+s.
+MLI_FI half8 acc_to_frag(const f32x16& v, int s) {
+  half8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (f16)v[8 * s + j];
+  return o;
+}
+
+MLI_FI float softplus100(float x) {
+  // torch.nn.functional.softplus(x, beta=100, threshold=20) with hardware exp/log.
+  const float t = x * 100.0f;
+  const float sp = __logf(1.0f + __expf(t)) * 0.01f;
+  return t > 20.0f ? x : sp;
+}
+
+MLI_FI float sigmoidf_acc(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// Real spherical harmonics, levels = 3 (projects/neuralangelo/utils/spherical_harmonics.py:47-84).
+MLI_FI void sh16(float x, float y, float z, float* o) {
+  const float C0 = 0.28209479177387814f, C1 = 0.4886025119029199f;
+  const float C20 = 1.0925484305920792f, C21 = -1.0925484305920792f, C22 = 0.31539156525252005f,
+              C23 = -1.0925484305920792f, C24 = 0.5462742152960396f;
+  const float C30 = -0.5900435899266435f, C31 = 2.890611442640554f, C32 = -0.4570457994644658f,
+              C33 = 0.3731763325901154f, C34 = -0.4570457994644658f, C35 = 1.445305721320277f,
+              C36 = -0.5900435899266435f;
+  const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+  o[0] = C0;
+  o[1] = -C1 * y;
+  o[2] = C1 * z;
+  o[3] = -C1 * x;
+  o[4] = C20 * xy;
+  o[5] = C21 * yz;
+  o[6] = C22 * (2.0f * zz - xx - yy);
+  o[7] = C23 * xz;
+  o[8] = C24 * (xx - yy);
+  o[9] = C30 * y * (3.0f * xx - yy);
+  o[10] = C31 * xy * z;
+  o[11] = C32 * y * (4.0f * zz - xx - yy);
+  o[12] = C33 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy);
+  o[13] = C34 * x * (4.0f * zz - xx - yy);
+  o[14] = C35 * z * (xx - yy);
+  o[15] = C36 * x * (xx - 3.0f * yy);
+}
+
+// Opaque copy: defeats loop-invariant hoisting of address arithmetic built from x (the
+// hoisted values otherwise stay live across the whole loop and spill).
+MLI_FI int opaque_s(int x) {
+  asm volatile("" : "+s"(x));
+  return x;
+}
+MLI_FI int opaque_v(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+#define MLI_LAUNCH_CHECK() return (int)hipGetLastError()

@@ -1,0 +1,153 @@
+// Parameter-side kernels: weight-norm fold + fp16 MFMA chunk packing, the weight-norm
+// backward / grad assembly into the flat grad buffer, AdamW, fp16 shadow cast.
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- pack
+// One thread per 16-byte fragment block (t, q, lane) of one layer (blockIdx.y), plus
+// 32 bias writers per n-tile (q == k_steps).  W = g * v / ||v||_row (torch weight_norm).
+__global__ __launch_bounds__(256) void pack_kernel(const mli_pack_layer* layers, uint8_t* dst) {
+  const mli_pack_layer& L = layers[blockIdx.y];
+  const int per_tile = (L.k_steps + 1) * 64;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= L.n_tiles * per_tile) return;
+  const int t = gid / per_tile, rem = gid - t * per_tile;
+  const int q = rem >> 6, lane = rem & 63;
+  uint8_t* chunk = dst + L.dst_offset + (size_t)t * L.chunk_stride;
+  const int rows_src = L.n_out, cols_src = L.k_ref;
+  auto wnorm_scale = [&](int row) {  // g[row] / ||v[row, :]||
+    const float* vr = L.v + (size_t)row * cols_src;
+    float ss = 0.f;
+    for (int k = 0; k < cols_src; ++k) ss += vr[k] * vr[k];
+    return L.g[row] / sqrtf(ss);
+  };
+  if (q == L.k_steps) {  // bias block: [h][i] in accumulator order
+    if (lane >= 32) return;
+    const int hh = lane >> 4, i = lane & 15;
+    const int n = 32 * t + acc_row(i, hh);
+    float b = 0.f;
+    if (!L.transpose && L.bias && n < rows_src) b = L.bias[n];
+    reinterpret_cast<float*>(chunk + L.k_steps * 1024)[hh * 16 + i] = b;
+    return;
+  }
+  const int rl = lane & 31, hh = lane >> 5;
+  const int n = 32 * t + rl;
+  half8 out;
+  float sc_row = 0.f;
+  if (!L.transpose && n < rows_src) sc_row = wnorm_scale(n);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int kk = L.kmode[q] ? k_acc(q, hh, j) : k_nat(q, hh, j);
+    const int src = L.kmap[kk];
+    float w = 0.f;
+    if (src >= 0) {
+      if (!L.transpose) {
+        if (n < rows_src) w = L.v[(size_t)n * cols_src + src] * sc_row;
+      } else {
+        // A = W^T: row n indexes W's columns, packed k indexes W's rows (src)
+        if (n < cols_src) w = L.v[(size_t)src * cols_src + n] * wnorm_scale(src);
+      }
+    }
+    out[j] = (f16)w;
+  }
+  *reinterpret_cast<half8*>(chunk + q * 1024 + lane * 16) = out;
+}
+
+// ---------------------------------------------------------------- grad assembly
+// dW_ref[n][c] = dW_pack[n][kinv[c]] * inv_scale; weight-norm backward:
+//   dg[n] = sum_c dW_ref[n][c] * v[n][c] / ||v_n||
+//   dv[n][c] = g[n] / ||v_n|| * (dW_ref[n][c] - dg[n] * v[n][c] / ||v_n||)
+__global__ __launch_bounds__(256) void assemble_kernel(const mli_assemble_layer* layers, float inv_scale) {
+  const mli_assemble_layer& L = layers[blockIdx.y];
+  const int n = blockIdx.x;
+  if (n >= L.n_out) return;
+  __shared__ float red[2][256];
+  const int tid = threadIdx.x;
+  const float* vr = L.v + (size_t)n * L.k_ref;
+  float ss = 0.f, dot = 0.f;
+  for (int c = tid; c < L.k_ref; c += 256) {
+    const float d = L.dw[(size_t)n * L.k_pack + L.kinv[c]] * inv_scale;
+    ss += vr[c] * vr[c];
+    dot += d * vr[c];
+  }
+  red[0][tid] = ss;
+  red[1][tid] = dot;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) {
+      red[0][tid] += red[0][tid + s];
+      red[1][tid] += red[1][tid + s];
+    }
+    __syncthreads();
+  }
+  const float nrm = sqrtf(red[0][0]);
+  const float dg = red[1][0] / nrm;
+  const float gs = L.g[n] / nrm;
+  for (int c = tid; c < L.k_ref; c += 256) {
+    const float d = L.dw[(size_t)n * L.k_pack + L.kinv[c]] * inv_scale;
+    L.grad_v[(size_t)n * L.k_ref + c] = gs * (d - dg * vr[c] / nrm);
+  }
+  if (tid == 0) {
+    L.grad_g[n] = dg;
+    L.grad_b[n] = L.db[n] * inv_scale;
+  }
+}
+
+// ---------------------------------------------------------------- AdamW (torch semantics)
+__global__ __launch_bounds__(256) void adamw_kernel(mli_adamw_args a, float bc1, float bc2_sqrt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  float p = a.p[i];
+  const float g = a.g[i];
+  p = p * (1.0f - a.lr * a.weight_decay);
+  float m = a.m[i], v = a.v[i];
+  m = m + (g - m) * (1.0f - a.beta1);
+  v = v * a.beta2 + (g * g) * (1.0f - a.beta2);
+  const float denom = sqrtf(v) / bc2_sqrt + a.eps;
+  p = p - (a.lr / bc1) * (m / denom);
+  a.p[i] = p;
+  a.m[i] = m;
+  a.v[i] = v;
+}
+
+__global__ __launch_bounds__(256) void cast_kernel(mli_cast_args a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  a.dst[i] = __builtin_bit_cast(uint16_t, (f16)a.src[i]);
+}
+
+}  // namespace
+
+extern "C" int mli_pack(const mli_pack_args* a, mli_stream_t s) {
+  // the host passes max threads over layers through n_layers' descriptors; size generously
+  const int max_threads = 8 * (19 + 1) * 64;
+  hipLaunchKernelGGL(pack_kernel, dim3((max_threads + 255) / 256, a->n_layers), dim3(256), 0,
+                     (hipStream_t)s, a->layers, a->dst);
+  MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_grad_assemble(const mli_assemble_args* a, mli_stream_t s) {
+  hipLaunchKernelGGL(assemble_kernel, dim3(256, a->n_layers), dim3(256), 0, (hipStream_t)s,
+                     a->layers, a->inv_scale);
+  MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_adamw(const mli_adamw_args* a, mli_stream_t s) {
+  if (a->n <= 0) return 0;
+  const float bc1 = 1.0f - powf(a->beta1, (float)a->step);
+  const float bc2 = 1.0f - powf(a->beta2, (float)a->step);
+  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)((a->n + 255) / 256)), dim3(256), 0, (hipStream_t)s,
+                     *a, bc1, sqrtf(bc2));
+  MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_cast_f16(const mli_cast_args* a, mli_stream_t s) {
+  if (a->n <= 0) return 0;
+  hipLaunchKernelGGL(cast_kernel, dim3((unsigned)((a->n + 255) / 256)), dim3(256), 0, (hipStream_t)s, *a);
+  MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_abi_version(void) { return MLI_ABI_VERSION; }
+
+extern "C" const char* mli_error_string(int code) { return hipGetErrorString((hipError_t)code); }

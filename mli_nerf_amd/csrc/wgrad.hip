@@ -1,0 +1,170 @@
+// Weight / bias gradients of the colour heads: dW = dZ^T X, db = sum_s dZ (split-K MFMA).
+//
+// Replaces the autograd dW/db GEMMs of nn.Linear inside MLPwithSkipConnection
+// (projects/nerf/utils/nerf_util.py:186-196).  Both operands are feature-major fp16 rows
+// [rows][S] (samples contiguous), so the reduction axis (samples) is the contiguous one for
+// both MFMA operands: a plain NT GEMM.  Each workgroup owns a BM x BN output tile and a
+// k_split-sample slice; partial sums land in the fp32 outputs by atomics (few: one per
+// output element per slice).
+#include "common.h"
+
+namespace {
+
+constexpr int MAXJOBS = 16;
+constexpr int BK = 64;                 // samples per k-step (4 MFMA k-steps)
+constexpr int ROWB = BK * 2 + 16;      // LDS row stride in bytes (16 B pad: conflict-free b128)
+
+struct Job {
+  const uint16_t* a; const uint16_t* b;
+  int M, K;
+  float* dw; float* db;
+  int tiles_n, tile_base;
+};
+
+struct KArgs {
+  Job jobs[MAXJOBS];
+  int n_jobs, S, k_split, n_split;
+};
+
+// Rows [t*ROWS, t*ROWS + ROWS) x BK samples from k, 8 x 16 B per row, rows clamped to n_rows.
+template <int ROWS, int LOADS>
+MLI_FI void stage_load(u32x4 (&st)[LOADS], const uint16_t* __restrict__ base, int n_rows, int t,
+                       size_t S, int k, int tid) {
+#pragma unroll
+  for (int u = 0; u < LOADS; ++u) {
+    const int id = u * 512 + tid, row = min(id >> 3, ROWS - 1), col = id & 7;
+    const int gr = min(t * ROWS + row, n_rows - 1);
+    st[u] = *reinterpret_cast<const u32x4*>(base + gr * S + k + col * 8);
+  }
+}
+
+template <int ROWS, int LOADS>
+MLI_FI void stage_store(const u32x4 (&st)[LOADS], uint8_t* lds, int tid) {
+#pragma unroll
+  for (int u = 0; u < LOADS; ++u) {
+    const int id = u * 512 + tid, row = id >> 3, col = id & 7;
+    if (ROWS * 8 >= (u + 1) * 512 || row < ROWS) *reinterpret_cast<u32x4*>(lds + row * ROWB + col * 16) = st[u];
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(512) void wgrad_kernel(KArgs ka) {
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t* la = lds;
+  uint8_t* lb = lds + BM * ROWB;
+  // locate job / tile / split
+  const int bid = blockIdx.x;
+  Job J = ka.jobs[0];
+#pragma unroll
+  for (int j = 1; j < MAXJOBS; ++j)
+    if (j < ka.n_jobs && bid >= ka.jobs[j].tile_base) J = ka.jobs[j];
+  const int local = bid - J.tile_base;
+  const int split = local % ka.n_split;
+  const int tt = local / ka.n_split;
+  const int tm = tt / J.tiles_n, tn = tt - tm * J.tiles_n;
+  const int k0 = split * ka.k_split;
+  const int k1 = min(ka.S, k0 + ka.k_split);
+  if (k0 >= k1) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave - wm * WN;
+  const int h = lane >> 5, rl = lane & 31;
+  const size_t S = ka.S;
+
+  // staging map: 8 x 16 B per row of BK samples
+  constexpr int A_LOADS = (BM * 8 + 511) / 512, B_LOADS = (BN * 8 + 511) / 512;
+  u32x4 sa[A_LOADS], sb[B_LOADS];
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  const bool do_bias = (J.db != nullptr) && tn == 0;
+  float bsum = 0.f;  // row (tid >> 1) of the A tile, half (tid & 1)
+
+  stage_load<BM, A_LOADS>(sa, J.a, J.M, tm, S, k0, tid);
+  stage_load<BN, B_LOADS>(sb, J.b, J.K, tn, S, k0, tid);
+  for (int kk = k0; kk < k1; kk += BK) {
+    __syncthreads();
+    stage_store<BM, A_LOADS>(sa, la, tid);
+    stage_store<BN, B_LOADS>(sb, lb, tid);
+    __syncthreads();
+    {  // prefetch the next k-step (clamped: the last iteration reloads a valid slice)
+      const int kn = min(kk + BK, k1 - BK);
+      stage_load<BM, A_LOADS>(sa, J.a, J.M, tm, S, kn, tid);
+      stage_load<BN, B_LOADS>(sb, J.b, J.K, tn, S, kn, tid);
+    }
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      half8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[i] = *reinterpret_cast<const half8*>(la + (wm * TM * 32 + i * 32 + rl) * ROWB + ks * 32 + h * 16);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[j] = *reinterpret_cast<const half8*>(lb + (wn * TN * 32 + j * 32 + rl) * ROWB + ks * 32 + h * 16);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(fa[i], fb[j], acc[i][j]);
+    }
+    if (do_bias && (tid >> 1) < BM) {
+      const half8* rowp = reinterpret_cast<const half8*>(la + (tid >> 1) * ROWB + (tid & 1) * 64);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const half8 v = rowp[u];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bsum += (float)v[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = tm * BM + wm * TM * 32 + i * 32 + acc_row(e, h);
+        const int col = tn * BN + wn * TN * 32 + j * 32 + rl;
+        if (row < J.M && col < J.K) atomicAdd(J.dw + (size_t)row * J.K + col, acc[i][j][e]);
+      }
+  if (do_bias) {
+    bsum += __shfl_xor(bsum, 1);
+    const int row = tm * BM + (tid >> 1);
+    if ((tid & 1) == 0 && (tid >> 1) < BM && row < J.M) atomicAdd(J.db + row, bsum);
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch(const mli_wgrad_args* a, bool thin, hipStream_t s) {
+  KArgs ka;
+  ka.S = a->S;
+  ka.k_split = a->k_split;
+  ka.n_split = (a->S + a->k_split - 1) / a->k_split;
+  int n = 0, base = 0;
+  for (int i = 0; i < a->n_jobs; ++i) {
+    const mli_wgrad_job& j = a->jobs[i];
+    if ((j.M <= 32) != thin) continue;
+    if (n == MAXJOBS) return (int)hipErrorInvalidValue;
+    Job& J = ka.jobs[n++];
+    J.a = j.a_rows; J.b = j.b_rows; J.M = j.M; J.K = j.K; J.dw = j.dw; J.db = j.db;
+    J.tiles_n = (j.K + BN - 1) / BN;
+    J.tile_base = base;
+    base += ((j.M + BM - 1) / BM) * J.tiles_n * ka.n_split;
+  }
+  ka.n_jobs = n;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN>), dim3(base), dim3(512), (BM + BN) * ROWB, s, ka);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int mli_wgrad(const mli_wgrad_args* a, mli_stream_t s) {
+  if (a->S % BK != 0 || a->k_split % BK != 0) return (int)hipErrorInvalidValue;
+  int e = launch<256, 128, 4, 2>(a, false, (hipStream_t)s);
+  if (e) return e;
+  return launch<32, 256, 1, 8>(a, true, (hipStream_t)s);
+}

@@ -1,0 +1,314 @@
+"""Device-side orchestration of the stage-b render path on libmli_hip.so.
+
+One ``RenderEngine`` per device/rank.  It owns every buffer the kernels use (allocated by
+PyTorch, handed to the C ABI as raw pointers on the current stream) and runs:
+
+  rays -> coarse samples -> sdf -> 4 x (section pdf -> fine samples -> sdf) -> merge
+       -> field (sdf + 4 taps + h0) -> heads (feat + rgb/o_r/o_s) -> NeuS composite
+and, in training, the backward of the composite into the heads, the dX chain, the weight
+gradients and the weight-norm backward into one flat fp32 gradient buffer.
+
+Reference call stack mirrored: NeuralLumen/model.py:113-131 (forward),
+:232-336 (render_rays_lumen), :338-403 (render_rays_object_lumen),
+neuralangelo/model.py:449-515 (sampling, NeuS alphas).
+"""
+import ctypes as C
+import math
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from . import layout
+from .hashgrid import level_table, normal_eps
+
+
+class PathConfig:
+    """Hot-path knobs, filled from the reference config tree (see model.py)."""
+
+    def __init__(self, n_coarse=64, n_fine=16, n_hier=4, white_bg=True, bounding="sphere",
+                 aabb=(-1, -1, -1, 1, 1, 1), outside_val=1000.0, anneal_end=0.1, log2T=22,
+                 levels=16, min_logres=5, max_logres=11):
+        self.n_coarse, self.n_fine, self.n_hier = n_coarse, n_fine, n_hier
+        self.white_bg, self.bounding, self.aabb = white_bg, bounding, tuple(float(x) for x in aabb)
+        self.outside_val, self.anneal_end = outside_val, anneal_end
+        self.log2T, self.levels, self.min_logres, self.max_logres = log2T, levels, min_logres, max_logres
+
+    @property
+    def n_samples(self):
+        return self.n_coarse + self.n_fine * self.n_hier
+
+
+def _grid_levels(cfg):
+    table, total = level_table(cfg.levels, cfg.log2T, cfg.min_logres, cfg.max_logres)
+    g = L.GridLevels()
+    for i, (scale, res, size, off) in enumerate(table):
+        g.scale[i], g.res[i], g.size[i], g.offset[i] = scale, res, size, off
+        g.modmagic[i] = layout.fastmod_magic(size)
+    return g, total
+
+
+def _to_device_structs(structs, device):
+    raw = b"".join(bytes(s) for s in structs)
+    return torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
+
+
+class RenderEngine:
+    def __init__(self, cfg, device):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.levels, self.table_entries = _grid_levels(cfg)
+        eps64 = normal_eps(cfg.levels, cfg.min_logres, cfg.max_logres) / np.sqrt(3)
+        self.eps = float(np.float32(eps64))
+        self.grad_den = float(np.float32(4.0 * eps64))
+        self.hess_den = float(np.float32(eps64 ** 2))
+        self.table16 = None
+        self.wsdf = torch.empty(C.sizeof(C.c_uint8) * (65536 + 5 * 1024 + 16), dtype=torch.uint8,
+                                device=self.device)
+        self.fplan, fbytes = layout.fwd_plan()
+        self.bplan, bbytes = layout.bwd_plan()
+        self.wfwd = torch.empty(fbytes, dtype=torch.uint8, device=self.device)
+        self.wbwd = torch.empty(bbytes, dtype=torch.uint8, device=self.device)
+        self._kmaps = []  # keep host kmap tensors alive
+        self.tlayout, self.n_train = layout.trainable_layout()
+        self.toff = {name: (off, shape) for name, shape, off in self.tlayout}
+        self._bufs = {}
+        self.u_fine = (C.c_float * 64)(*(layout.u_fine(cfg.n_fine) + [2.0] * (64 - cfg.n_fine)))
+        self._pack_descs = None
+
+    # ------------------------------------------------------------------ parameters
+    def load_sdf(self, params_flat, v0, g0, b0, w_sdf, b_sdf):
+        """Frozen geometry (stage b): fp16 shadow of the hash table + packed layer 0."""
+        assert params_flat.numel() == self.table_entries * 8, (params_flat.numel(), self.table_entries)
+        self.table16 = torch.empty(params_flat.numel(), dtype=torch.float16, device=self.device)
+        L.call("mli_cast_f16", L.CastArgs(L.ptr(params_flat), L.ptr(self.table16), params_flat.numel()))
+        L.call("mli_pack_sdf", L.PackSdfArgs(L.ptr(v0), L.ptr(g0), L.ptr(b0), L.ptr(w_sdf), L.ptr(b_sdf),
+                                             L.ptr(self.wsdf)))
+
+    def _descs(self, plan, tensors):
+        descs = []
+        for p in plan:
+            km = torch.from_numpy(p["kmap"].astype(np.int16)).to(self.device)
+            kmode = torch.from_numpy(p["kmode"].astype(np.uint8)).to(self.device)
+            self._kmaps += [km, kmode]
+            v, g, b = tensors(p["prefix"])
+            descs.append(L.PackLayer(L.ptr(v), L.ptr(g), L.ptr(b), p["n_out"], p["k_ref"], p["transpose"],
+                                     p["n_tiles"], p["k_steps"], L.ptr(km), L.ptr(kmode), p["dst_offset"],
+                                     p["chunk_stride"]))
+        return descs
+
+    def pack_heads(self, flat, sdf_l1):
+        """Weight-norm fold + fp16 fragment packing of SDF layer 1 and the three heads
+        (forward image) and of the transposed head layers (backward image)."""
+        def tensors(prefix):
+            if prefix == "neural_sdf.mlp.linears.1":
+                return sdf_l1
+            return tuple(self.param_view(flat, prefix + s) for s in (".weight_v", ".weight_g", ".bias"))
+        key = (flat.data_ptr(), sdf_l1[0].data_ptr())
+        if self._pack_descs is None or self._pack_descs[0] != key:
+            self._kmaps = []
+            fd = _to_device_structs(self._descs(self.fplan, tensors), self.device)
+            bd = _to_device_structs(self._descs(self.bplan, tensors), self.device)
+            self._pack_descs = (key, fd, bd, len(self.fplan), len(self.bplan))
+        _, fd, bd, nf, nb = self._pack_descs
+        L.call("mli_pack", L.PackArgs(nf, L.ptr(fd), L.ptr(self.wfwd)))
+        L.call("mli_pack", L.PackArgs(nb, L.ptr(bd), L.ptr(self.wbwd)))
+
+    def param_view(self, flat, name):
+        off, shape = self.toff[name]
+        n = int(np.prod(shape))
+        return flat[off:off + n].view(*shape)
+
+    # ------------------------------------------------------------------ buffers
+    def _buf(self, name, shape, dtype=torch.float32):
+        t = self._bufs.get(name)
+        n = int(np.prod(shape))
+        if t is None or t.numel() < n or t.dtype != dtype:
+            t = torch.empty(n, dtype=dtype, device=self.device)
+            self._bufs[name] = t
+        return t[:n].view(*shape)
+
+    # ------------------------------------------------------------------ forward
+    @torch.no_grad()
+    def rays(self, pose, intr, pose_light, ray_idx, W, R=None, first_pixel=0):
+        """pose/intr/pose_light [1,3,4]/[1,3,3]/[1,3,4]; ray_idx [1,R] int64 or None."""
+        c2w = _invert(pose[0]).contiguous()
+        c2w_l = _invert(pose_light[0]).contiguous()
+        kinv = intr[0].inverse().contiguous()
+        R = R if ray_idx is None else ray_idx.shape[-1]
+        ridx = None if ray_idx is None else ray_idx.reshape(-1).to(torch.int64).contiguous()
+        out = dict(center=self._buf("center", (R, 3)), ray_unit=self._buf("ray_unit", (R, 3)),
+                   ray_norm=self._buf("ray_norm", (R,)), pts_light=self._buf("pts_light", (R, 3)),
+                   near=self._buf("near", (R,)), far=self._buf("far", (R,)),
+                   outside=self._buf("outside", (R,), torch.uint8))
+        aabb = (C.c_float * 6)(*self.cfg.aabb)
+        L.call("mli_rays", L.RaysArgs(L.ptr(kinv), L.ptr(c2w), L.ptr(c2w_l), L.ptr(ridx), first_pixel, R, W,
+                                      1 if self.cfg.bounding == "box" else 0, aabb,
+                                      L.ptr(out["center"]), L.ptr(out["ray_unit"]), L.ptr(out["ray_norm"]),
+                                      L.ptr(out["pts_light"]), L.ptr(out["near"]), L.ptr(out["far"]),
+                                      L.ptr(out["outside"])))
+        out["_keep"] = (c2w, c2w_l, kinv, ridx)
+        return out
+
+    def _sdf(self, rays, dists, n_per_ray, out, mode=0, grad=None, hess=None, h0=None):
+        R = rays["center"].shape[0]
+        L.call("mli_sdf", L.SdfArgs(mode, R, n_per_ray, L.ptr(rays["center"]), L.ptr(rays["ray_unit"]),
+                                    L.ptr(dists), L.ptr(rays["outside"]), L.ptr(self.table16), self.levels,
+                                    L.ptr(self.wsdf), self.eps, self.grad_den, self.hess_den,
+                                    self.cfg.outside_val, 1 if hess is not None else 0, L.ptr(out),
+                                    L.ptr(grad), L.ptr(hess), L.ptr(h0)))
+
+    @torch.no_grad()
+    def sample(self, rays, u=None):
+        """sample_dists_all (neuralangelo/model.py:449-465) -> dists [N][R]."""
+        cfg = self.cfg
+        R = rays["center"].shape[0]
+        Nc, Nf, H = cfg.n_coarse, cfg.n_fine, cfg.n_hier
+        N = cfg.n_samples
+        d0 = self._buf("d_coarse", (Nc, R))
+        uu = None if u is None else u.reshape(R, Nc).contiguous()
+        L.call("mli_sample_coarse", L.SampleCoarseArgs(L.ptr(rays["near"]), L.ptr(rays["far"]), L.ptr(uu),
+                                                       R, Nc, L.ptr(d0)))
+        s0 = self._buf("s_coarse", (Nc, R))
+        self._sdf(rays, d0, Nc, s0)
+        da, sa, na = d0, s0, Nc
+        db = sb = None
+        nb = 0
+        for h in range(H):
+            dm = self._buf("d_m%d" % (h & 1), (na + nb, R))
+            sm = self._buf("s_m%d" % (h & 1), (na + nb, R))
+            f = self._buf("d_f%d" % (h & 1), (Nf, R))
+            L.call("mli_sample_fine", L.SampleFineArgs(R, L.ptr(da), L.ptr(sa), na, L.ptr(db), L.ptr(sb), nb,
+                                                       L.ptr(dm), L.ptr(sm), Nf, float(64 * 2 ** h),
+                                                       C.cast(self.u_fine, C.c_void_p), L.ptr(f)))
+            sf = None
+            if h < H - 1:
+                sf = self._buf("s_f%d" % (h & 1), (Nf, R))
+                self._sdf(rays, f, Nf, sf)
+            da, sa, na, db, sb, nb = dm, sm, na + nb, f, sf, Nf
+        dists = self._buf("dists", (N, R))
+        L.call("mli_sample_fine", L.SampleFineArgs(R, L.ptr(da), None, na, L.ptr(db), None, nb, L.ptr(dists),
+                                                   None, 0, 0.0, None, None))
+        return dists
+
+    @torch.no_grad()
+    def field(self, rays, dists, training):
+        N, R = dists.shape
+        S = N * R
+        sdf = self._buf("sdf", (N, R))
+        grad = self._buf("grad", (N, R, 3))
+        hess = self._buf("hess", (N, R, 3)) if training else None
+        h0 = self._buf("h0", (S * 256,), torch.float16)
+        self._sdf(rays, dists, N, sdf, mode=1, grad=grad, hess=hess, h0=h0)
+        return dict(sdf=sdf, grad=grad, hess=hess, h0=h0)
+
+    @torch.no_grad()
+    def heads(self, rays, dists, fld, training):
+        N, R = dists.shape
+        S = N * R
+        y = self._buf("y", (N, R, 8))
+        feat = self._buf("feat", (S * 256,), torch.float16)
+        x0T = xT = masks = None
+        if training:
+            x0T = self._buf("x0T", (layout.K0, S), torch.float16)
+            xT = self._buf("xT", (3, 4, 256, S), torch.float16)
+            masks = self._buf("masks", (3, 4, S // 32, 64, 4), torch.int32)
+        L.call("mli_rgb_fwd", L.RgbFwdArgs(R, N, L.ptr(rays["center"]), L.ptr(rays["ray_unit"]),
+                                           L.ptr(rays["pts_light"]), L.ptr(dists), L.ptr(fld["grad"]),
+                                           L.ptr(fld["h0"]), L.ptr(self.wfwd), L.ptr(y), L.ptr(feat),
+                                           L.ptr(x0T), L.ptr(xT), L.ptr(masks)))
+        return dict(y=y, x0T=x0T, xT=xT, masks=masks)
+
+    @torch.no_grad()
+    def composite(self, rays, dists, fld, hd, s_var, progress, training):
+        N, R = dists.shape
+        out = dict(weights=self._buf("weights", (N, R)),
+                   rgb=torch.empty(R, 3, device=self.device), o_r=torch.empty(R, 3, device=self.device),
+                   o_s=torch.empty(R, 1, device=self.device), o_re=torch.empty(R, 3, device=self.device))
+        if not training:
+            out.update(opacity=torch.empty(R, 1, device=self.device),
+                       gradient=torch.empty(R, 3, device=self.device),
+                       depth=torch.empty(R, 1, device=self.device))
+        anneal = min(progress / self.cfg.anneal_end, 1.0)
+        L.call("mli_composite_fwd", L.CompositeArgs(R, N, L.ptr(dists), L.ptr(rays["far"]), L.ptr(rays["ray_unit"]),
+                                                    L.ptr(rays["ray_norm"]), L.ptr(fld["sdf"]), L.ptr(fld["grad"]),
+                                                    L.ptr(hd["y"]), L.ptr(s_var), float(anneal),
+                                                    1 if self.cfg.white_bg else 0, L.ptr(out["weights"]),
+                                                    L.ptr(out["rgb"]), L.ptr(out["o_r"]), L.ptr(out["o_s"]),
+                                                    L.ptr(out["o_re"]), L.ptr(out.get("opacity")),
+                                                    L.ptr(out.get("gradient")), L.ptr(out.get("depth"))))
+        return out
+
+    def render(self, data, s_var, progress, training, u=None, W=512):
+        rays = self.rays(data["pose"], data["intr"], data["pose_light"], data["ray_idx"], W)
+        dists = self.sample(rays, u)
+        fld = self.field(rays, dists, training)
+        hd = self.heads(rays, dists, fld, training)
+        comp = self.composite(rays, dists, fld, hd, s_var, progress, training)
+        return rays, dists, fld, hd, comp
+
+    # ------------------------------------------------------------------ backward
+    @torch.no_grad()
+    def backward(self, st, d_rgb, d_o_r, d_o_s, d_o_re, flat, sdf_l1, grad_out):
+        """Gradient of the loss w.r.t. the trainable head parameters into grad_out (flat)."""
+        rays, dists, fld, hd, comp = st
+        N, R = dists.shape
+        S = N * R
+        scale = float(2.0 ** round(math.log2(max(R, 1)) + 2))
+        dz4 = self._buf("dz4", (N, R, 8))
+        c = lambda t: None if t is None else t.contiguous()  # noqa: E731
+        L.call("mli_composite_bwd", L.CompositeBwdArgs(R, N, L.ptr(comp["weights"]), L.ptr(hd["y"]),
+                                                       L.ptr(comp["o_r"]), L.ptr(comp["o_s"]), L.ptr(c(d_rgb)),
+                                                       L.ptr(c(d_o_r)), L.ptr(c(d_o_s)), L.ptr(c(d_o_re)),
+                                                       scale, L.ptr(dz4)))
+        dzT = self._buf("dzT", (3, 4, 256, S), torch.float16)
+        dz4T = self._buf("dz4T", (3, 4, S), torch.float16)
+        L.call("mli_rgb_bwd", L.RgbBwdArgs(R, N, L.ptr(dz4), L.ptr(self.wbwd), L.ptr(hd["masks"]), L.ptr(dzT),
+                                           L.ptr(dz4T)))
+        # weight gradients (packed-k space), zeroed then accumulated by split-K atomics
+        sizes = []
+        for hdx, (name, k_in, k_out) in enumerate(layout.HEADS):
+            sizes += [(256, layout.K0), (256, 256), (256, 256), (256, 256), (k_out, 256)]
+        total = sum(m * k + m for m, k in sizes)
+        dwbuf = self._buf("dw", (total,))
+        dwbuf.zero_()
+        jobs, assemble, off = [], [], 0
+        self._kinv_keep = []
+        for hdx, (name, k_in, k_out) in enumerate(layout.HEADS):
+            for li in range(5):
+                m, k = sizes[hdx * 5 + li]
+                dw = dwbuf[off:off + m * k]
+                db = dwbuf[off + m * k:off + m * k + m]
+                off += m * k + m
+                if li == 0:
+                    a_rows, b_rows = dzT[hdx, 0], hd["x0T"]
+                elif li < 4:
+                    a_rows, b_rows = dzT[hdx, li], hd["xT"][hdx, li - 1]
+                else:
+                    a_rows, b_rows = dz4T[hdx], hd["xT"][hdx, 3]
+                jobs.append(L.WgradJob(L.ptr(a_rows), L.ptr(b_rows), m, k, L.ptr(dw), L.ptr(db)))
+                pre = layout.param_prefix(name, li)
+                v = self.param_view(flat, pre + ".weight_v")
+                g = self.param_view(flat, pre + ".weight_g")
+                k_ref = v.shape[1]
+                kinv = layout.head_kinv(name, k_ref) if li == 0 else np.arange(k_ref, dtype=np.int16)
+                kinv_t = torch.from_numpy(kinv.astype(np.int16)).to(self.device)
+                self._kinv_keep.append(kinv_t)
+                assemble.append(L.AssembleLayer(L.ptr(dw), L.ptr(db), L.ptr(v), L.ptr(g), m, k_ref, k,
+                                                L.ptr(kinv_t), L.ptr(self.param_view(grad_out, pre + ".weight_v")),
+                                                L.ptr(self.param_view(grad_out, pre + ".weight_g")),
+                                                L.ptr(self.param_view(grad_out, pre + ".bias")), None))
+        job_arr = (L.WgradJob * len(jobs))(*jobs)
+        k_split = 32768 if S >= 32768 * 4 else max(64, (S // 4) // 64 * 64)
+        L.call("mli_wgrad", L.WgradArgs(S, len(jobs), C.cast(job_arr, C.c_void_p), k_split))
+        ad = _to_device_structs(assemble, self.device)
+        self._assemble_keep = ad
+        L.call("mli_grad_assemble", L.AssembleArgs(len(assemble), L.ptr(ad), 1.0 / scale))
+        return grad_out
+
+
+def _invert(pose):
+    """camera.Pose.invert (projects/nerf/utils/camera.py:46-52) on a [3,4] tensor."""
+    rot, trans = pose[:, :3], pose[:, 3:]
+    rt = rot.transpose(0, 1)
+    return torch.cat([rt, -(rt @ trans)], dim=1)

@@ -1,0 +1,126 @@
+"""Packing plans shared by the host and the kernels (see include/mli_hip.h).
+
+Packed-k order of the head layer-0 input (MLI_HEAD_K0 = 304 rows):
+    0..255   feat (SDF layer-1 softplus output), accumulator order
+    256..258 p, 259..261 normal, 262..271 zero pad          (k-step 16, NAT order)
+    272..287 SH16(light position)                           (k-step 17, NAT order)
+    288..303 SH16(view direction)                           (k-step 18, NAT order)
+Reference column order of each head's first Linear (NeuralLumen/utils/modules.py:149-151):
+    mlp   (rgb): [p 3, view 16, n 3, feat 256, light 16] = 294
+    mlp_r (o_r): [p 3, n 3, feat 256]                    = 262
+    mlp_s (o_s): [p 3, n 3, feat 256, light 16]          = 278
+"""
+import numpy as np
+
+HEADS = (("mlp", 294, 3), ("mlp_r", 262, 3), ("mlp_s", 278, 1))
+HIDDEN = 256
+K0 = 304
+KS0 = 19
+NAT, ACC = 0, 1
+
+
+def chunk_bytes(k_steps):
+    return k_steps * 1024 + 128
+
+
+def head_kmap(name):
+    """Packed k (0..303) -> reference input column (-1 = zero)."""
+    km = -np.ones(K0, dtype=np.int16)
+    feat0 = {"mlp": 22, "mlp_r": 6, "mlp_s": 6}[name]
+    n0 = {"mlp": 19, "mlp_r": 3, "mlp_s": 3}[name]
+    light0 = {"mlp": 278, "mlp_r": None, "mlp_s": 262}[name]
+    view0 = {"mlp": 3, "mlp_r": None, "mlp_s": None}[name]
+    km[0:256] = feat0 + np.arange(256)
+    km[256:259] = np.arange(3)
+    km[259:262] = n0 + np.arange(3)
+    if light0 is not None:
+        km[272:288] = light0 + np.arange(16)
+    if view0 is not None:
+        km[288:304] = view0 + np.arange(16)
+    return km
+
+
+def head_kinv(name, k_ref):
+    km = head_kmap(name)
+    inv = np.zeros(k_ref, dtype=np.int16)
+    for kk, c in enumerate(km):
+        if c >= 0:
+            inv[c] = kk
+    return inv
+
+
+def ident_kmap(n, pad_to):
+    km = -np.ones(pad_to, dtype=np.int16)
+    km[:n] = np.arange(n)
+    return km
+
+
+def param_prefix(head, layer):
+    return "neural_rgb.%s.linears.%d" % (head, layer)
+
+
+def trainable_layout():
+    """Flat fp32 buffer layout of the stage-b trainable parameters (partial_grad neural_rgb,
+    NeuralLumen/trainer.py:44-54): [(name, shape, offset)]."""
+    out, off = [], 0
+    for head, k_in, k_out in HEADS:
+        dims = [k_in] + [HIDDEN] * 4 + [k_out]
+        for li in range(5):
+            pre = param_prefix(head, li)
+            for suffix, shape in (("weight_v", (dims[li + 1], dims[li])), ("weight_g", (dims[li + 1], 1)),
+                                  ("bias", (dims[li + 1],))):
+                out.append((pre + "." + suffix, shape, off))
+                off += int(np.prod(shape))
+    return out, off
+
+
+def fwd_plan():
+    """Chunk sequence of the forward weight image, in kernel consumption order.
+    Each entry: dict(param prefix, n_out, k_ref, transpose, n_tiles, k_steps, kmap, kmode)."""
+    plan = [dict(prefix="neural_sdf.mlp.linears.1", n_out=256, k_ref=256, transpose=0, n_tiles=8,
+                 k_steps=16, kmap=ident_kmap(256, 256), kmode=np.full(16, ACC, np.uint8))]
+    for head, k_in, k_out in HEADS:
+        kmode0 = np.array([ACC] * 16 + [NAT] * 3, np.uint8)
+        plan.append(dict(prefix=param_prefix(head, 0), n_out=256, k_ref=k_in, transpose=0, n_tiles=8,
+                         k_steps=KS0, kmap=head_kmap(head), kmode=kmode0))
+        for li in (1, 2, 3):
+            plan.append(dict(prefix=param_prefix(head, li), n_out=256, k_ref=256, transpose=0,
+                             n_tiles=8, k_steps=16, kmap=ident_kmap(256, 256),
+                             kmode=np.full(16, ACC, np.uint8)))
+        plan.append(dict(prefix=param_prefix(head, 4), n_out=k_out, k_ref=256, transpose=0, n_tiles=1,
+                         k_steps=16, kmap=ident_kmap(256, 256), kmode=np.full(16, ACC, np.uint8)))
+    return _with_offsets(plan)
+
+
+def bwd_plan():
+    """Transposed weights of the dX chain: per head W4^T (k over the outputs, 1 k-step),
+    W3^T, W2^T, W1^T."""
+    plan = []
+    for head, k_in, k_out in HEADS:
+        plan.append(dict(prefix=param_prefix(head, 4), n_out=k_out, k_ref=256, transpose=1, n_tiles=8,
+                         k_steps=1, kmap=ident_kmap(k_out, 16), kmode=np.full(1, ACC, np.uint8)))
+        for li in (3, 2, 1):
+            plan.append(dict(prefix=param_prefix(head, li), n_out=256, k_ref=256, transpose=1,
+                             n_tiles=8, k_steps=16, kmap=ident_kmap(256, 256),
+                             kmode=np.full(16, ACC, np.uint8)))
+    return _with_offsets(plan)
+
+
+def _with_offsets(plan):
+    off = 0
+    for p in plan:
+        p["chunk_stride"] = chunk_bytes(p["k_steps"])
+        p["dst_offset"] = off
+        off += p["n_tiles"] * p["chunk_stride"]
+    return plan, off
+
+
+def u_fine(n_fine):
+    """Midpoint quantiles exactly as nerf_util.sample_dists_from_pdf builds them (:55-56)."""
+    import torch
+    grid = torch.linspace(0, 1, n_fine + 1)
+    return (0.5 * (grid[:-1] + grid[1:])).tolist()
+
+
+def fastmod_magic(d):
+    return ((1 << 64) // d + 1) & ((1 << 64) - 1)

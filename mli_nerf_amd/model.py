@@ -1,0 +1,276 @@
+"""Drop-in ``Model`` for the NeuralLumen stage-b render path on MI355X.
+
+Mirrors the reference plugin surface (``cfg.model.type`` -> ``Model(cfg_model, cfg_data)``,
+imaginaire/trainers/base.py:118-119; NeuralLumen/model.py:17-131):
+
+* module / parameter names and shapes match the reference state dict, so checkpoints
+  load with ``load_state_dict`` (keys ``neural_sdf.tcnn_encoding.params``,
+  ``neural_sdf.mlp.linears.{0,1}.{weight_g,weight_v,bias}``, ``neural_sdf.mlp.linear_sdf.*``,
+  ``neural_rgb.{mlp,mlp_r,mlp_s}.linears.{0..4}.*``, ``s_var``);
+* ``forward(data)`` returns the reference output dict (rgb, o_r, o_s, o_re, opacity, outside,
+  dists, weights, gradient, gradients, hessians) with rgb/o_r/o_s/o_re differentiable w.r.t.
+  the trainable ``neural_rgb`` parameters (stage b, NeuralLumen/trainer.py:44-54);
+* ``inference(data)`` renders the full image in ``rand_rays_val`` chunks (:60-111).
+
+All compute runs in libmli_hip.so; the trainable parameters live in ONE flat fp32 buffer
+(``self.flat``), the named ``nn.Parameter``s are views into it.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import layout
+from .engine import PathConfig, RenderEngine
+from .hashgrid import GRID_DEFAULTS, level_table
+
+
+def _cfg_get(node, path, default=None):
+    cur = node
+    for key in path.split("."):
+        if cur is None or not hasattr(cur, key) and not (isinstance(cur, dict) and key in cur):
+            return default
+        cur = cur[key] if isinstance(cur, dict) else getattr(cur, key)
+    return cur
+
+
+def path_config_from(cfg_model, cfg_data):
+    ns = cfg_model.render.num_samples
+    hg = cfg_model.object.sdf.encoding.hashgrid
+    box = _cfg_get(cfg_data, "bounding_type", "unit_sphere") == "box"
+    inside_out = bool(_cfg_get(cfg_model, "object.sdf.mlp.inside_out", False))
+    return PathConfig(n_coarse=ns.coarse, n_fine=ns.fine, n_hier=cfg_model.render.num_sample_hierarchy,
+                      white_bg=bool(cfg_model.background.white), bounding="box" if box else "sphere",
+                      aabb=tuple(_cfg_get(cfg_data, "bounding_box_aabb", (-1, -1, -1, 1, 1, 1))),
+                      outside_val=1000.0 * (-1 if inside_out else 1),
+                      anneal_end=float(cfg_model.object.s_var.anneal_end),
+                      log2T=int(hg.dict_size), levels=int(cfg_model.object.sdf.encoding.levels),
+                      min_logres=int(hg.min_logres), max_logres=int(hg.max_logres))
+
+
+class WNLinear(torch.nn.Module):
+    """Parameter holder with torch weight_norm names (nerf_util.py:176-178)."""
+
+    def __init__(self, v, g, b):
+        super().__init__()
+        self.weight_g, self.weight_v, self.bias = v_param(g), v_param(v), v_param(b)
+
+
+class PlainLinear(torch.nn.Module):
+    def __init__(self, w, b):
+        super().__init__()
+        self.weight, self.bias = v_param(w), v_param(b)
+
+
+def v_param(t, requires_grad=False):
+    return torch.nn.Parameter(t, requires_grad=requires_grad)
+
+
+class _MLP(torch.nn.Module):
+    def __init__(self, linears):
+        super().__init__()
+        self.linears = torch.nn.ModuleList(linears)
+
+
+class _Encoding(torch.nn.Module):
+    def __init__(self, n_params):
+        super().__init__()
+        self.params = torch.nn.Parameter(torch.zeros(n_params), requires_grad=False)
+
+
+class NeuralSDF(torch.nn.Module):
+    """Parameter-compatible stand-in for neuralangelo/utils/modules.py:NeuralSDF (frozen in
+    stage b).  Attributes the trainers poke are kept (normal_eps, resolutions, ...)."""
+
+    def __init__(self, pcfg):
+        super().__init__()
+        _, total = level_table(pcfg.levels, pcfg.log2T, pcfg.min_logres, pcfg.max_logres)
+        self.tcnn_encoding = _Encoding(total * 8)
+        k0 = 3 + pcfg.levels * 8
+        mlp = _MLP([WNLinear(torch.zeros(256, k0), torch.ones(256, 1), torch.zeros(256)),
+                    WNLinear(torch.zeros(256, 256), torch.ones(256, 1), torch.zeros(256))])
+        mlp.linear_sdf = PlainLinear(torch.zeros(1, 256), torch.zeros(1))
+        self.mlp = mlp
+        g = np.exp((np.log(2 ** pcfg.max_logres) - np.log(2 ** pcfg.min_logres)) / (pcfg.levels - 1))
+        self.growth_rate = g
+        self.resolutions = [int(np.floor(2 ** pcfg.min_logres * g ** lv)) + 1 for lv in range(pcfg.levels)]
+        self.normal_eps = 1.0 / self.resolutions[-1]
+        self.active_levels = self.anneal_levels = pcfg.levels
+        self.warm_up_end = 0
+
+    def set_normal_epsilon(self):
+        """modules.py:102-107 (coarse-to-fine disabled in stage b)."""
+        self.normal_eps = 1.0 / self.resolutions[-1]
+
+    def set_active_levels(self, current_iter=None):
+        self.active_levels = self.anneal_levels = len(self.resolutions)
+
+
+class LumenRGB(torch.nn.Module):
+    """Parameter layout of NeuralLumen/utils/modules.py:LumenRGB mode 'rgb_r_s'; the
+    tensors are views of the model's flat trainable buffer."""
+
+    def __init__(self, flat):
+        super().__init__()
+        lay = {name: (shape, off) for name, shape, off in layout.trainable_layout()[0]}
+
+        def view(name):
+            shape, off = lay[name]
+            return flat[off:off + int(np.prod(shape))].view(*shape)
+
+        for head, _, _ in layout.HEADS:
+            lins = []
+            for li in range(5):
+                pre = layout.param_prefix(head, li)
+                lins.append(WNLinear(view(pre + ".weight_v"), view(pre + ".weight_g"), view(pre + ".bias")))
+                for p in lins[-1].parameters():
+                    p.requires_grad_(True)
+            setattr(self, head, _MLP(lins))
+
+
+class _RenderHeads(torch.autograd.Function):
+    """Forward: the whole stage-b render on the GPU.  Backward: composite -> heads dX chain ->
+    dW GEMMs -> weight-norm backward, producing the gradient of the flat trainable buffer."""
+
+    @staticmethod
+    def forward(ctx, flat, model, data, u, progress, training):
+        eng = model.engine
+        st = eng.render(data, model.s_var.detach(), progress, training, u=u, W=model.image_width)
+        ctx.state = st
+        ctx.model = model
+        model._last_state = st
+        comp = st[4]
+        return comp["rgb"], comp["o_r"], comp["o_s"], comp["o_re"]
+
+    @staticmethod
+    def backward(ctx, d_rgb, d_o_r, d_o_s, d_o_re):
+        model = ctx.model
+        grad = torch.zeros_like(model.flat)
+        model.engine.backward(ctx.state, d_rgb, d_o_r, d_o_s, d_o_re, model.flat, model._sdf_l1(), grad)
+        ctx.state = None
+        return grad, None, None, None, None, None
+
+
+class Model(torch.nn.Module):
+    def __init__(self, cfg_model, cfg_data):
+        super().__init__()
+        self.cfg_model, self.cfg_data = cfg_model, cfg_data
+        self.pcfg = path_config_from(cfg_model, cfg_data)
+        self.image_size_train = list(cfg_data.train.image_size)
+        self.image_size_val = list(cfg_data.val.image_size)
+        self.rand_rays_val = int(_cfg_get(cfg_model, "render.rand_rays_val", cfg_model.render.rand_rays))
+        self.white_background = self.pcfg.white_bg
+        self.outside_val = self.pcfg.outside_val
+        self.anneal_end = self.pcfg.anneal_end
+        self.progress = 0.0
+        self.stratified = bool(cfg_model.render.stratified)
+        self.neural_sdf = NeuralSDF(self.pcfg)
+        n_train = layout.trainable_layout()[1]
+        self.register_buffer("flat", torch.zeros(n_train), persistent=False)
+        self.flat.requires_grad_(True)
+        self.neural_rgb = LumenRGB(self.flat)
+        self.s_var = torch.nn.Parameter(torch.tensor(float(cfg_model.object.s_var.init_val)),
+                                        requires_grad=False)
+        if self.pcfg.bounding == "box":
+            self.bounding_box_aabb = torch.tensor(self.pcfg.aabb)
+        self.engine = None
+        self._sdf_version = None
+        self.image_width = self.image_size_train[1]
+
+    # -------------------------------------------------------------- parameter plumbing
+    def device(self):
+        return self.flat.device
+
+    def _apply(self, fn, recurse=True):
+        super()._apply(fn, recurse)
+        # re-point the neural_rgb parameter views at the (possibly moved) flat buffer
+        flat = self.flat.detach().requires_grad_(True)
+        self._buffers["flat"] = flat
+        lay = {name: (shape, off) for name, shape, off in layout.trainable_layout()[0]}
+        for name, p in self.neural_rgb.named_parameters():
+            shape, off = lay["neural_rgb." + name]
+            p.data = flat.data[off:off + int(np.prod(shape))].view(*shape)
+        self.engine = None
+        self._sdf_version = None
+        return self
+
+    def _sdf_l1(self):
+        l1 = self.neural_sdf.mlp.linears[1]
+        return (l1.weight_v.detach(), l1.weight_g.detach().reshape(-1), l1.bias.detach())
+
+    def prepare(self):
+        """(Re)build the device weight images: SDF (once, frozen) + heads (every step)."""
+        if self.engine is None:
+            self.engine = RenderEngine(self.pcfg, self.flat.device)
+        sdf = self.neural_sdf
+        ver = tuple(p._version for p in sdf.parameters()) + tuple(p.data_ptr() for p in sdf.parameters())
+        if ver != self._sdf_version:
+            l0 = sdf.mlp.linears[0]
+            self.engine.load_sdf(sdf.tcnn_encoding.params.detach(), l0.weight_v.detach(),
+                                 l0.weight_g.detach().reshape(-1), l0.bias.detach(),
+                                 sdf.mlp.linear_sdf.weight.detach().reshape(-1), sdf.mlp.linear_sdf.bias.detach())
+            self._sdf_version = ver
+        self.engine.pack_heads(self.flat.detach(), self._sdf_l1())
+
+    # -------------------------------------------------------------- reference API
+    def get_param_groups(self, cfg_optim):
+        """NeuralLumen/model.py:422-438 (partial_training keywords)."""
+        keywords = _cfg_get(cfg_optim, "partial_training", None)
+        if keywords is None:
+            return self.parameters()
+        return [p for n, p in self.named_parameters() if any(k in n for k in keywords)]
+
+    def forward(self, data, u=None):
+        """NeuralLumen/model.py:113-118 -> render_pixels_lumen; ``u`` injects the stratified
+        uniforms (nerf_util.py:33) for parity runs."""
+        self.prepare()
+        stratified = self.stratified and self.training
+        if stratified and u is None:
+            u = torch.rand(1, data["ray_idx"].shape[-1], self.pcfg.n_coarse, device=self.flat.device)
+        if not stratified:
+            u = None
+        self.image_width = self.image_size_train[1]
+        rgb, o_r, o_s, o_re = _RenderHeads.apply(self.flat, self, data, u, self.progress, self.training)
+        rays, dists, fld, hd, comp = self._last_state
+        N, R = dists.shape
+        out = dict(rgb=rgb[None], o_r=o_r[None], o_s=o_s[None], o_re=o_re[None],
+                   outside=rays["outside"].bool().view(1, R, 1),
+                   dists=dists.t().reshape(1, R, N, 1),
+                   weights=comp["weights"].t().reshape(1, R, N, 1),
+                   gradients=fld["grad"].permute(1, 0, 2).reshape(1, R, N, 3),
+                   hessians=None if fld["hess"] is None else fld["hess"].permute(1, 0, 2).reshape(1, R, N, 3),
+                   opacity=None, gradient=None)
+        if not self.training:
+            out["opacity"] = comp["opacity"][None]
+            out["gradient"] = comp["gradient"][None]
+            out["depth"] = comp["depth"][None]
+        return out
+
+    @torch.no_grad()
+    def inference(self, data):
+        """NeuralLumen/model.py:60-111: full image in rand_rays_val chunks, eval branch."""
+        self.eval()
+        self.prepare()
+        H, W = self.image_size_val
+        n_pix = H * W
+        self.image_width = W
+        chunks = []
+        for start in range(0, n_pix, self.rand_rays_val):
+            R = min(self.rand_rays_val, n_pix - start)
+            ridx = torch.arange(start, start + R, device=self.flat.device)[None]
+            d = dict(pose=data["pose"], intr=data["intr"], pose_light=data["pose_light"], ray_idx=ridx)
+            st = self.engine.render(d, self.s_var.detach(), self.progress, False, u=None, W=W)
+            comp = st[4]
+            chunks.append({k: comp[k].clone() for k in ("rgb", "o_r", "o_s", "o_re", "opacity", "gradient", "depth")})
+        out = {k: torch.cat([c[k] for c in chunks], 0)[None] for k in chunks[0]}
+        rot = data["pose"][..., :3, :3]
+        normal_cam = -out["gradient"] @ rot.transpose(-1, -2)
+
+        def full(x):
+            return x.unflatten(1, (H, W)).moveaxis(-1, 1)
+        out.update(rgb_map=full(out["rgb"]), opacity_map=full(out["opacity"]), depth_map=full(out["depth"]),
+                   normal_map=full(normal_cam))
+        for k in ("o_r", "o_s", "o_re"):
+            out[k + "_map"] = full(out[k])
+        return out

@@ -1,0 +1,183 @@
+"""Stage-b trainer surface (drop-in for projects.NeuralLumen.trainer on the hot path).
+
+Mirrors NeuralLumen/trainer.py:20-214 + neuralangelo/trainer.py:23-112 +
+imaginaire/trainers/base.py (train_step, _get_total_loss, checkpoint layout):
+
+* losses: 3 x L1 render, PSNR, eikonal, curvature, intrinsic (global min/max weight maps),
+  residual regulariser (NeuralLumen/trainer.py:133-149, utils.py:142-174,
+  neuralangelo/utils/misc.py:74-90), total = sum weight_k * loss_k (base.py:534-544);
+* optimiser: AdamW (lr 1e-3, wd 1e-2) on the trainable neural_rgb parameters only, run as
+  ONE fused HIP kernel over the flat parameter buffer; LR schedule two_steps_with_warmup
+  (neuralangelo/utils/misc.py:28-54);
+* multi-GPU: one process per GPU, gradients averaged with ONE all-reduce of the flat
+  gradient buffer (3.2 MB) over RCCL (DDP semantics, get_trainer.py:80-88);
+* checkpoints: {"model", "optim", "sched", "epoch", "iteration"} with ``module.``-prefixed
+  model keys and ``latest_checkpoint.txt`` (imaginaire/trainers/base.py:570-607).
+"""
+import os
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib as L
+
+
+def intrinsic_loss(o_r, o_s, ref, sha, cert, ranges, factors=(1.0, 1.0)):
+    """NeuralLumen/utils/utils.py:142-162."""
+    def rescale(x, lo, hi):
+        return lo + (x - x.min()) / torch.clamp(x.max() - x.min(), min=1e-6) * (hi - lo)
+    w_sha = rescale(sha.detach(), *ranges[0])
+    w_vis = rescale(cert.detach(), *ranges[1])
+    w_ref = torch.minimum(w_vis, w_sha)
+    return (torch.abs(o_r - ref) * w_ref).mean() * factors[0] + (torch.abs(o_s - sha) * w_sha).mean() * factors[1]
+
+
+def regularize_re_loss(o_re, f_neg=10.0, f_pos=1.0, e_pos=1.0):
+    """NeuralLumen/utils/utils.py:165-174."""
+    zero = torch.zeros_like(o_re)
+    neg = torch.where(o_re < 0.0, o_re, zero)
+    pos = torch.where(o_re >= 0.0, o_re, zero)
+    return torch.abs(neg).mean() * f_neg + torch.pow(pos, e_pos).mean() * f_pos
+
+
+def eikonal_loss(gradients, outside):
+    """neuralangelo/utils/misc.py:74-81."""
+    err = ((gradients.norm(dim=-1) - 1.0) ** 2).nan_to_num(nan=0.0, posinf=0.0, neginf=0.0)
+    return (err * (~outside).float()).mean()
+
+
+def curvature_loss(hessians, outside):
+    """neuralangelo/utils/misc.py:83-90."""
+    lap = hessians.sum(dim=-1).abs().nan_to_num(nan=0.0, posinf=0.0, neginf=0.0)
+    return (lap * (~outside).float()).mean()
+
+
+def stage_b_losses(out, data, weights, ranges=((0.0, 1.0), (0.0, 1.0)), re_factors=(10.0, 1.0, 1.0)):
+    losses = {}
+    if "render" in weights:
+        losses["render"] = F.l1_loss(out["rgb"], data["image_sampled"]) * 3
+    if "eikonal" in weights:
+        losses["eikonal"] = eikonal_loss(out["gradients"], out["outside"])
+    if "curvature" in weights and out.get("hessians") is not None:
+        losses["curvature"] = curvature_loss(out["hessians"], out["outside"])
+    if "intrinsic" in weights:
+        losses["intrinsic"] = intrinsic_loss(out["o_r"], out["o_s"], data["pseudo_ref_sampled"],
+                                             data["pseudo_sha_sampled"],
+                                             data["pseudo_visibility_certainty_sampled"], ranges)
+    if "regularize_re" in weights:
+        losses["regularize_re"] = regularize_re_loss(out["o_re"], *re_factors)
+    total = sum(losses[k] * weights[k] for k in weights if k in losses)
+    psnr = -10 * torch.log10(F.mse_loss(out["rgb"].detach(), data["image_sampled"]))
+    return total, losses, psnr
+
+
+def two_steps_with_warmup(it, warm_up_end=5000, two_steps=(300000, 400000), gamma=10.0):
+    """neuralangelo/utils/misc.py:43-52."""
+    if it < warm_up_end:
+        return it / warm_up_end
+    if it > two_steps[1]:
+        return 1.0 / gamma ** 2
+    if it > two_steps[0]:
+        return 1.0 / gamma
+    return 1.0
+
+
+class FusedAdamW:
+    """torch.optim.AdamW semantics over the model's flat trainable buffer, one HIP launch."""
+
+    def __init__(self, flat, lr=1e-3, weight_decay=1e-2, betas=(0.9, 0.999), eps=1e-8):
+        self.flat = flat
+        self.lr, self.wd, self.betas, self.eps = lr, weight_decay, betas, eps
+        self.m = torch.zeros_like(flat.detach())
+        self.v = torch.zeros_like(flat.detach())
+        self.step_count = 0
+
+    def step(self, grad, lr):
+        self.step_count += 1
+        L.call("mli_adamw", L.AdamwArgs(L.ptr(self.flat.detach()), L.ptr(grad), L.ptr(self.m), L.ptr(self.v),
+                                        self.flat.numel(), float(lr), self.betas[0], self.betas[1], self.eps,
+                                        self.wd, self.step_count))
+
+    def state_dict(self):
+        return {"step": self.step_count, "exp_avg": self.m, "exp_avg_sq": self.v, "lr": self.lr,
+                "weight_decay": self.wd, "betas": self.betas, "eps": self.eps}
+
+    def load_state_dict(self, sd):
+        self.step_count = sd["step"]
+        self.m.copy_(sd["exp_avg"])
+        self.v.copy_(sd["exp_avg_sq"])
+
+
+class Trainer:
+    """Minimal stage-b trainer: ``train_step(data)`` = forward + loss + backward + AdamW."""
+
+    def __init__(self, cfg, model, world_size=1):
+        self.cfg = cfg
+        self.model = model
+        self.weights = {k: v for k, v in cfg.trainer.loss_weight.items() if v}
+        p = cfg.trainer.para_intrinsic_loss
+        self.ranges = (tuple(p["weight_map_range_shading"]), tuple(p["weight_map_range_visibility"]))
+        q = cfg.trainer.para_regularize_re_loss
+        self.re_factors = (q["factor_negative"], q["factor_positive"], q["exponent_positive"])
+        o = cfg.optim
+        self.optim = FusedAdamW(model.flat, lr=o.params.lr, weight_decay=o.params.weight_decay)
+        self.sched = o.sched
+        self.current_iteration = 0
+        self.current_epoch = 0
+        self.world_size = world_size
+        self.losses, self.metrics = {}, {}
+
+    def lr(self):
+        s = self.sched
+        return self.optim.lr * two_steps_with_warmup(self.current_iteration, s.warm_up_end,
+                                                     tuple(s.two_steps), s.gamma)
+
+    def _start_of_iteration(self):
+        """neuralangelo/trainer.py:65-76: progress restarts at 0 in stage b (no resume)."""
+        self.model.progress = self.current_iteration / self.cfg.max_iter
+        self.model.neural_sdf.set_normal_epsilon()
+
+    def train_step(self, data, u=None):
+        self._start_of_iteration()
+        self.model.train()
+        if self.model.flat.grad is not None:
+            self.model.flat.grad = None
+        out = self.model(data, u=u)
+        total, losses, psnr = stage_b_losses(out, data, self.weights, self.ranges, self.re_factors)
+        total.backward()
+        grad = self.model.flat.grad
+        if self.world_size > 1:
+            import torch.distributed as dist
+            dist.all_reduce(grad, op=dist.ReduceOp.SUM)
+            grad.div_(self.world_size)
+        self.optim.step(grad, self.lr())
+        self.current_iteration += 1
+        self.losses = {k: v.detach() for k, v in losses.items()}
+        self.losses["total"] = total.detach()
+        self.metrics["psnr"] = psnr
+        return out
+
+    # ------------------------------------------------------------ checkpoint layout
+    def save_checkpoint(self, logdir):
+        """imaginaire/trainers/base.py:570-607 file naming + latest_checkpoint.txt."""
+        os.makedirs(logdir, exist_ok=True)
+        name = "epoch_{:05}_iteration_{:09}_checkpoint.pt".format(self.current_epoch, self.current_iteration)
+        sd = {"module." + k: v for k, v in self.model.state_dict().items()}
+        torch.save(dict(model=sd, optim=self.optim.state_dict(), sched={"last_epoch": self.current_iteration},
+                        epoch=self.current_epoch, iteration=self.current_iteration), os.path.join(logdir, name))
+        with open(os.path.join(logdir, "latest_checkpoint.txt"), "w") as f:
+            f.write(name + "\n")
+        return os.path.join(logdir, name)
+
+    def load_checkpoint(self, path, resume=True):
+        if path.endswith(".txt"):
+            with open(path) as f:
+                path = os.path.join(os.path.dirname(path), f.readline().strip())
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        model_sd = {k[len("module."):] if k.startswith("module.") else k: v for k, v in sd["model"].items()}
+        res = self.model.load_state_dict(model_sd, strict=False)
+        if resume and "optim" in sd and "exp_avg" in sd["optim"]:
+            self.optim.load_state_dict(sd["optim"])
+            self.current_iteration = sd.get("iteration", 0)
+            self.current_epoch = sd.get("epoch", 0)
+        return res

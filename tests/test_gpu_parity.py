@@ -1,0 +1,204 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle on identical inputs.
+
+Each stage is fed the GPU's own upstream outputs (copied to the CPU), so a failure
+localises to one kernel.  Tolerances are stated per stage:
+
+* rays / bounds / coarse dists: fp32 elementwise, 1e-5 relative;
+* hash-grid encode: indices bit-exact (the oracle is given the same fp16-rounded table),
+  values 1e-5 (fp32 accumulation order);
+* SDF (fp16 MFMA operands, fp32 accumulate, fp32 p-term): |sdf| 2e-3;
+  4-tap gradients are sdf differences / (4 eps = 5.6e-4), i.e. the sdf tolerance
+  amplified 1.8e3x: normals compared by angle (< 2 degrees) and |grad| by 2 %;
+* heads (fp16 MFMA, 5 layers): sigmoid outputs 5e-3 abs;
+* composite given identical inputs: 1e-4;
+* end to end (stage-b forward, hotdog R=64): rgb / o_r / o_s 2e-2 abs max, mean 2e-3,
+  PSNR of the difference >= 40 dB;
+* weight gradients: cosine similarity >= 0.99 per tensor, relative norm error <= 5 %.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mli_nerf_amd import synthetic
+from mli_nerf_amd.configs import preset
+from oracle import hashgrid as o_hash, render as o_render
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def build(config="syn_hotdog_b", R=64, Nc=16, Nf=4, H=4, log2T=14, s_var=3.0):
+    from mli_nerf_amd.model import Model
+    cfg = preset(config, rays=R, n_coarse=Nc, n_fine=Nf, n_hier=H, log2T=log2T)
+    model = Model(cfg.model, cfg.data)
+    sd = synthetic.make_state_dict(log2T=log2T, s_var=s_var)
+    model.load_state_dict(sd)
+    model = model.to(DEV)
+    Hh, W = cfg.data.train.image_size
+    data = synthetic.make_batch(R, H=Hh, W=W, frame=3)
+    pcfg = o_render.PathCfg(n_coarse=Nc, n_fine=Nf, n_hier=H, log2T=log2T,
+                            white_bg=bool(cfg.model.background.white),
+                            bounding="box" if cfg.data.bounding_type == "box" else "sphere",
+                            aabb=tuple(cfg.data.get("bounding_box_aabb", (-1, -1, -1, 1, 1, 1))))
+    return model, sd, data, pcfg, (Hh, W)
+
+
+def to_dev(data):
+    return {k: v.to(DEV) for k, v in data.items()}
+
+
+def fp16_table_sd(sd):
+    """State dict whose hash table holds the fp16-rounded values the GPU gathers."""
+    sd = dict(sd)
+    sd["neural_sdf.tcnn_encoding.params"] = sd["neural_sdf.tcnn_encoding.params"].half().float()
+    return sd
+
+
+def test_hashgrid_encode_full_table():
+    _need_gpu()
+    from mli_nerf_amd import _lib as L
+    from mli_nerf_amd.engine import _grid_levels, PathConfig
+    cfg = PathConfig(log2T=22)
+    levels, total = _grid_levels(cfg)
+    g = torch.Generator().manual_seed(11)
+    params = (torch.rand(total * 8, generator=g) * 0.2 - 0.1).half()
+    # in-range points plus out-of-range ones (outside rays: negative coords wrap in uint32)
+    x = torch.cat([torch.rand(3000, 3, generator=g), torch.rand(1000, 3, generator=g) * 1.6 - 0.3])
+    out = torch.empty(x.shape[0], 128, device=DEV)
+    xd, pd = x.to(DEV).contiguous(), params.to(DEV)
+    L.call("mli_hashgrid_fwd", L.HashgridArgs(L.ptr(xd), L.ptr(pd), levels, x.shape[0], L.ptr(out)))
+    torch.cuda.synchronize()
+    table, _ = o_hash.level_table()
+    ref = o_hash.encode(x, params.float(), table)
+    err = (out.cpu() - ref).abs().max().item()
+    print("hashgrid max err", err)
+    assert err < 1e-5
+
+
+def test_stagewise_forward():
+    _need_gpu()
+    model, sd, data, pcfg, (Hh, W) = build()
+    R = data["ray_idx"].shape[-1]
+    eng_data = to_dev(data)
+    model.train()
+    model.prepare()
+    eng = model.engine
+    sd16 = fp16_table_sd(sd)
+    # 1. rays + bounds
+    rays = eng.rays(eng_data["pose"], eng_data["intr"], eng_data["pose_light"], eng_data["ray_idx"], W)
+    center, ray = o_render.pixel_rays(data["pose"], data["intr"], data["ray_idx"], W, Hh)
+    ru = F.normalize(ray, dim=-1)
+    near, far, outside = o_render.sphere_bounds(center, ru)
+    torch.testing.assert_close(rays["center"].cpu(), center[0], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(rays["ray_unit"].cpu(), ru[0], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rays["near"].cpu(), near[0, :, 0], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(rays["far"].cpu(), far[0, :, 0], rtol=1e-5, atol=1e-5)
+    assert torch.equal(rays["outside"].cpu().bool(), outside[0, :, 0])
+    # GPU rays as the common input of the next stages
+    c_g = rays["center"].cpu()[None]
+    v_g = rays["ray_unit"].cpu()[None]
+    n_g, f_g = rays["near"].cpu()[None, :, None], rays["far"].cpu()[None, :, None]
+    out_g = rays["outside"].cpu().bool()[None, :, None]
+    # 2. sampling (identical uniforms)
+    u = torch.rand(1, R, pcfg.n_coarse)
+    dists = eng.sample(rays, u.to(DEV))
+    o_d = o_render.hierarchical_dists(sd16, pcfg, c_g, v_g, n_g, f_g, u)
+    d_err = (dists.t().cpu() - o_d[0, :, :, 0]).abs().max().item()
+    print("dists max err", d_err)
+    # 3. field at the GPU's dists
+    d_g = dists.t().cpu()[None, :, :, None]
+    pts = c_g[..., None, :] + v_g[..., None, :] * d_g
+    fld = eng.field(rays, dists, True)
+    o_s, o_feat = o_render.sdf_net(sd16, pcfg, pts, with_feat=True)
+    o_s = torch.where(out_g[..., None].expand_as(o_s), torch.full_like(o_s, 1000.0), o_s)
+    o_g, o_h = o_render.sdf_taps(sd16, pcfg, pts, o_s, True)
+    g_sdf = fld["sdf"].t().cpu()
+    g_grad = fld["grad"].permute(1, 0, 2).cpu()
+    sdf_err = (g_sdf - o_s[0, ..., 0]).abs().max().item()
+    cosang = F.cosine_similarity(g_grad, o_g[0], dim=-1).clamp(-1, 1)
+    ang = torch.rad2deg(torch.acos(cosang)).max().item()
+    nrm_rel = ((g_grad.norm(dim=-1) - o_g[0].norm(dim=-1)).abs() / o_g[0].norm(dim=-1)).max().item()
+    print("sdf max err %.3g  grad max angle %.3g deg  |grad| rel %.3g" % (sdf_err, ang, nrm_rel))
+    # 4. heads at the GPU's points / gradients
+    hd = eng.heads(rays, dists, fld, True)
+    y = hd["y"].permute(1, 0, 2).cpu()
+    normals = F.normalize(g_grad[None], dim=-1)
+    o_rgb, o_r, o_sh = o_render.rgb_heads(sd, pts, normals, v_g[..., None, :].expand_as(pts), o_feat,
+                                          rays["pts_light"].cpu()[None, :, None, :].expand_as(pts))
+    e_rgb = (y[..., 0:3] - o_rgb[0]).abs().max().item()
+    e_r = (y[..., 3:6] - o_r[0]).abs().max().item()
+    e_s = (y[..., 6:7] - o_sh[0]).abs().max().item()
+    print("heads max err rgb %.3g o_r %.3g o_s %.3g" % (e_rgb, e_r, e_s))
+    # 5. composite given identical inputs
+    s_var = model.s_var.detach()
+    comp = eng.composite(rays, dists, fld, hd, s_var, 0.0, True)
+    al = o_render.neus_alphas(s_var.cpu(), v_g, g_sdf[None, ..., None], g_grad[None], d_g, f_g, 0.0, 0.1)
+    w = o_render.exclusive_transmittance_weights(al)
+    w_err = (comp["weights"].t().cpu() - w[0, ..., 0]).abs().max().item()
+    rgb_ref = (y[None, ..., 0:3] * w).sum(2) + (1 - w.sum(2))
+    c_err = (comp["rgb"].cpu() - rgb_ref[0]).abs().max().item()
+    print("composite weights err %.3g rgb err %.3g" % (w_err, c_err))
+    assert sdf_err < 2e-3
+    assert ang < 2.0 and nrm_rel < 0.02
+    assert max(e_rgb, e_r, e_s) < 5e-3
+    assert w_err < 1e-4 and c_err < 1e-4
+    assert d_err < 5e-3
+
+
+@pytest.mark.parametrize("case", ["hotdog_r64_n32", "hotdog_r64_n128", "pikachu_r32_n192", "savannah_r64_n32"])
+def test_end_to_end_forward_backward(case):
+    _need_gpu()
+    spec = {"hotdog_r64_n32": ("syn_hotdog_b", 64, 16, 4, 3.0),
+            "hotdog_r64_n128": ("syn_hotdog_b", 64, 64, 16, 6.0),
+            "pikachu_r32_n192": ("NRHints_Pikachu_b", 32, 64, 32, 3.0),
+            "savannah_r64_n32": ("rene_savannah_b", 64, 16, 4, 3.0)}[case]
+    config, R, Nc, Nf, s_var = spec
+    model, sd, data, pcfg, (Hh, W) = build(config, R, Nc, Nf, 4, 14, s_var)
+    model.train()
+    u = torch.rand(1, R, Nc)
+    out = model(to_dev(data), u=u.to(DEV))
+    total, losses, psnr = o_render.stage_b_losses(
+        {k: (v.cpu() if torch.is_tensor(v) else v) for k, v in out.items()}, data, pcfg)
+    total_gpu = _gpu_total(out, to_dev(data), pcfg)
+    total_gpu.backward()
+    g_flat = model.flat.grad.detach().cpu()
+    # oracle
+    sd_o = {k: v.clone().requires_grad_(k.startswith("neural_rgb")) for k, v in fp16_table_sd(sd).items()}
+    o_out = o_render.forward(sd_o, pcfg, data, u=u, training=True, progress=0.0, width=W, height=Hh)
+    o_total, o_losses, o_psnr = o_render.stage_b_losses(o_out, data, pcfg)
+    o_total.backward()
+    for key in ("rgb", "o_r", "o_s", "o_re"):
+        d = (out[key].detach().cpu() - o_out[key].detach()).abs()
+        psnr_d = -10 * math.log10(max(float((d ** 2).mean()), 1e-20))
+        print("%s %s max %.3g mean %.3g psnr(diff) %.1f dB" % (case, key, d.max(), d.mean(), psnr_d))
+        assert d.max() < 2e-2 and d.mean() < 2e-3 and psnr_d > 40, key
+    for k in ("render", "intrinsic", "regularize_re"):
+        a, b = losses[k].item(), o_losses[k].item()
+        assert abs(a - b) <= 1e-2 * max(abs(b), 1e-3) + 1e-4, (k, a, b)
+    lay = model.engine.tlayout
+    worst = 1.0
+    for name, shape, off in lay:
+        n = int(np.prod(shape))
+        g = g_flat[off:off + n].view(*shape)
+        o = sd_o[name].grad
+        cos = F.cosine_similarity(g.flatten(), o.flatten(), dim=0).item() if o.norm() > 0 else 1.0
+        rel = ((g - o).norm() / max(o.norm().item(), 1e-12)).item()
+        worst = min(worst, cos)
+        assert cos > 0.99 and rel < 0.05, (name, cos, rel)
+    print("%s grads: worst cosine %.5f" % (case, worst))
+
+
+def _gpu_total(out, data, pcfg):
+    """The same stage-b loss assembly as the trainer, evaluated on the GPU tensors."""
+    from mli_nerf_amd.trainer import stage_b_losses
+    total, _, _ = stage_b_losses(out, data, pcfg.loss_w, pcfg.intrinsic_ranges, pcfg.re_factors)
+    return total
