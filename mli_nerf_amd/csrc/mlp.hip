@@ -151,11 +151,16 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
       B[18][j] = (f16)(h ? v_hi : v_lo);
     }
     if (train) {
+      // feature-major rows 256..303 (k_nat order) from the fp32 sources
 #pragma unroll
-      for (int q = 16; q < 19; ++q)
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          a.x0T[(size_t)k_nat(q, h, j) * S + m] = __builtin_bit_cast(uint16_t, B[q][j]);
+      for (int j = 0; j < 8; ++j) {
+        const float v16 = h ? 0.f : e16[j];
+        const float v17 = h ? shl[8 + j] : shl[j];
+        const float v18 = h ? shv[8 + j] : shv[j];
+        a.x0T[(size_t)k_nat(16, h, j) * S + m] = __builtin_bit_cast(uint16_t, (f16)v16);
+        a.x0T[(size_t)k_nat(17, h, j) * S + m] = __builtin_bit_cast(uint16_t, (f16)v17);
+        a.x0T[(size_t)k_nat(18, h, j) * S + m] = __builtin_bit_cast(uint16_t, (f16)v18);
+      }
     }
   }
 
@@ -252,8 +257,9 @@ __global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
 #pragma unroll
         for (int j = 0; j < 3; ++j)
           if (j < no) {
-            z4[j] = (f16)dz[j];
-            a.dz4T[((size_t)hd * 4 + j) * S + m] = __builtin_bit_cast(uint16_t, z4[j]);
+            const f16 zj = (f16)dz[j];  // never bit_cast a vector element (yields element 0)
+            z4[j] = zj;
+            a.dz4T[((size_t)hd * 4 + j) * S + m] = __builtin_bit_cast(uint16_t, zj);
           }
       }
     }

@@ -75,6 +75,7 @@ class RenderEngine:
         self._bufs = {}
         self.u_fine = (C.c_float * 64)(*(layout.u_fine(cfg.n_fine) + [2.0] * (64 - cfg.n_fine)))
         self._pack_descs = None
+        self.trace = None  # set to a list to record per-round sampler outputs (debug/tests)
 
     # ------------------------------------------------------------------ parameters
     def load_sdf(self, params_flat, v0, g0, b0, w_sdf, b_sdf):
@@ -185,6 +186,9 @@ class RenderEngine:
             if h < H - 1:
                 sf = self._buf("s_f%d" % (h & 1), (Nf, R))
                 self._sdf(rays, f, Nf, sf)
+            if self.trace is not None:
+                self.trace.append(dict(merged=dm.clone(), merged_sdf=sm.clone(), fine=f.clone(),
+                                       fine_sdf=None if sf is None else sf.clone()))
             da, sa, na, db, sb, nb = dm, sm, na + nb, f, sf, Nf
         dists = self._buf("dists", (N, R))
         L.call("mli_sample_fine", L.SampleFineArgs(R, L.ptr(da), None, na, L.ptr(db), None, nb, L.ptr(dists),

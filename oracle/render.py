@@ -301,15 +301,18 @@ def neus_alphas(s_var, ray_unit, sdfs, grads, dists, far, progress, anneal_end):
     return ((cdf_prev - cdf_next) / (cdf_prev + 1e-5)).clip(0.0, 1.0)
 
 
-def render_rays(weights, cfg, center, ray_unit, pts_light, u=None, training=True, progress=0.0):
+def render_rays(weights, cfg, center, ray_unit, pts_light, u=None, training=True, progress=0.0,
+                dists=None):
     """NeuralLumen/model.py:232-336 render_rays_lumen + :338-403 render_rays_object_lumen,
-    network_mode 'rgb_r_s', no background NeRF, no light visibility."""
+    network_mode 'rgb_r_s', no background NeRF, no light visibility.  ``dists`` (test hook)
+    replaces the hierarchical sampler's output, to condition downstream comparisons."""
     with torch.no_grad():
         if cfg.bounding == "box":
             near, far, outside = aabb_bounds(center, ray_unit, cfg.aabb)
         else:
             near, far, outside = sphere_bounds(center, ray_unit)
-        dists = hierarchical_dists(weights, cfg, center, ray_unit, near, far, u)
+        if dists is None:
+            dists = hierarchical_dists(weights, cfg, center, ray_unit, near, far, u)
     pts = center[..., None, :] + ray_unit[..., None, :] * dists
     sdfs, feats = sdf_net(weights, cfg, pts, with_feat=True)
     sdfs = torch.where(outside[..., None].expand_as(sdfs), torch.full_like(sdfs, cfg.outside_val), sdfs)
@@ -336,7 +339,7 @@ def render_rays(weights, cfg, center, ray_unit, pts_light, u=None, training=True
     return out
 
 
-def forward(weights, cfg, data, u=None, training=True, progress=0.0, width=512, height=None):
+def forward(weights, cfg, data, u=None, training=True, progress=0.0, width=512, height=None, dists=None):
     """NeuralLumen/model.py:113-131 Model.forward -> render_pixels_lumen."""
     height = height or width
     center, ray = pixel_rays(data["pose"], data["intr"], data["ray_idx"], width, height)
@@ -344,7 +347,7 @@ def forward(weights, cfg, data, u=None, training=True, progress=0.0, width=512, 
     pts_light = light_points(data["pose_light"], height * width)
     bidx = torch.arange(ray.shape[0])[:, None].expand_as(data["ray_idx"])
     pts_light = pts_light[bidx, data["ray_idx"]]
-    return render_rays(weights, cfg, center, ray_unit, pts_light, u, training, progress)
+    return render_rays(weights, cfg, center, ray_unit, pts_light, u, training, progress, dists)
 
 
 # --------------------------------------------------------------------------------------

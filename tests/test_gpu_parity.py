@@ -7,12 +7,14 @@ localises to one kernel.  Tolerances are stated per stage:
 * hash-grid encode: indices bit-exact (the oracle is given the same fp16-rounded table),
   values 1e-5 (fp32 accumulation order);
 * SDF (fp16 MFMA operands, fp32 accumulate, fp32 p-term): |sdf| 2e-3;
-  4-tap gradients are sdf differences / (4 eps = 5.6e-4), i.e. the sdf tolerance
-  amplified 1.8e3x: normals compared by angle (< 2 degrees) and |grad| by 2 %;
+  4-tap gradients are sdf differences / (4 eps = 5.6e-4), i.e. the sdf error amplified
+  1.8e3x: where |grad| > 0.1 the normal angle p99 < 1 deg (max < 10) and |grad| p99 2 %;
+* sampler: each round fed the GPU's previous round, 1e-3 (unconditioned multi-round
+  comparisons are chaotic: inv_s = 512 sections amplify 1e-6 sdf noise);
 * heads (fp16 MFMA, 5 layers): sigmoid outputs 5e-3 abs;
 * composite given identical inputs: 1e-4;
-* end to end (stage-b forward, hotdog R=64): rgb / o_r / o_s 2e-2 abs max, mean 2e-3,
-  PSNR of the difference >= 40 dB;
+* end to end (stage-b forward): rgb / o_r / o_s mean abs 2e-3, PSNR of the difference
+  >= 40 dB, max 0.1 (a ray whose hierarchical samples move is allowed to differ);
 * weight gradients: cosine similarity >= 0.99 per tensor, relative norm error <= 5 %.
 """
 import math
@@ -38,6 +40,7 @@ def _need_gpu():
 
 def build(config="syn_hotdog_b", R=64, Nc=16, Nf=4, H=4, log2T=14, s_var=3.0):
     from mli_nerf_amd.model import Model
+    torch.manual_seed(1234)
     cfg = preset(config, rays=R, n_coarse=Nc, n_fine=Nf, n_hier=H, log2T=log2T)
     model = Model(cfg.model, cfg.data)
     sd = synthetic.make_state_dict(log2T=log2T, s_var=s_var)
@@ -108,12 +111,15 @@ def test_stagewise_forward():
     v_g = rays["ray_unit"].cpu()[None]
     n_g, f_g = rays["near"].cpu()[None, :, None], rays["far"].cpu()[None, :, None]
     out_g = rays["outside"].cpu().bool()[None, :, None]
-    # 2. sampling (identical uniforms)
+    # 2. sampling (identical uniforms), checked round by round: each oracle round is fed the
+    #    GPU's previous round (the inv_s = 64..512 section pdfs amplify 1e-6 sdf noise
+    #    chaotically across rounds, so an unconditioned end-state comparison is meaningless)
     u = torch.rand(1, R, pcfg.n_coarse)
+    eng.trace = []
     dists = eng.sample(rays, u.to(DEV))
-    o_d = o_render.hierarchical_dists(sd16, pcfg, c_g, v_g, n_g, f_g, u)
-    d_err = (dists.t().cpu() - o_d[0, :, :, 0]).abs().max().item()
-    print("dists max err", d_err)
+    trace, eng.trace = eng.trace, None
+    d_err = check_sampler_rounds(trace, dists, sd16, pcfg, c_g, v_g, n_g, f_g, u)
+    print("sampler per-round max err", d_err)
     # 3. field at the GPU's dists
     d_g = dists.t().cpu()[None, :, :, None]
     pts = c_g[..., None, :] + v_g[..., None, :] * d_g
@@ -124,10 +130,16 @@ def test_stagewise_forward():
     g_sdf = fld["sdf"].t().cpu()
     g_grad = fld["grad"].permute(1, 0, 2).cpu()
     sdf_err = (g_sdf - o_s[0, ..., 0]).abs().max().item()
+    # normals are sdf differences / 5.6e-4: compare where the field is well conditioned
+    # (|grad| > 0.1) and report the 99th percentile next to the max
     cosang = F.cosine_similarity(g_grad, o_g[0], dim=-1).clamp(-1, 1)
-    ang = torch.rad2deg(torch.acos(cosang)).max().item()
-    nrm_rel = ((g_grad.norm(dim=-1) - o_g[0].norm(dim=-1)).abs() / o_g[0].norm(dim=-1)).max().item()
-    print("sdf max err %.3g  grad max angle %.3g deg  |grad| rel %.3g" % (sdf_err, ang, nrm_rel))
+    well = o_g[0].norm(dim=-1) > 0.1
+    angs = torch.rad2deg(torch.acos(cosang))[well]
+    ang, ang99 = angs.max().item(), torch.quantile(angs, 0.99).item()
+    rel = ((g_grad.norm(dim=-1) - o_g[0].norm(dim=-1)).abs() / o_g[0].norm(dim=-1))[well]
+    nrm_rel = torch.quantile(rel, 0.99).item()
+    print("sdf max err %.3g  grad angle max %.3g p99 %.3g deg  |grad| rel p99 %.3g"
+          % (sdf_err, ang, ang99, nrm_rel))
     # 4. heads at the GPU's points / gradients
     hd = eng.heads(rays, dists, fld, True)
     y = hd["y"].permute(1, 0, 2).cpu()
@@ -148,10 +160,29 @@ def test_stagewise_forward():
     c_err = (comp["rgb"].cpu() - rgb_ref[0]).abs().max().item()
     print("composite weights err %.3g rgb err %.3g" % (w_err, c_err))
     assert sdf_err < 2e-3
-    assert ang < 2.0 and nrm_rel < 0.02
+    assert ang99 < 1.0 and ang < 10.0 and nrm_rel < 0.02
     assert max(e_rgb, e_r, e_s) < 5e-3
     assert w_err < 1e-4 and c_err < 1e-4
-    assert d_err < 5e-3
+    assert d_err < 1e-3
+
+
+def check_sampler_rounds(trace, dists_gpu, sd, pcfg, c, v, near, far, u):
+    R, Nf = c.shape[1], pcfg.n_fine
+    d = o_render.stratified_dists(near, far, pcfg.n_coarse, u)
+    s = o_render.sdf_net(sd, pcfg, c[..., None, :] + v[..., None, :] * d, False)[0]
+    worst = 0.0
+    for h, t in enumerate(trace):
+        nh = d.shape[2]
+        worst = max(worst, (t["merged"].view(nh, R).t().cpu() - d[0, :, :, 0]).abs().max().item())
+        fine = o_render.section_pdf_samples(d, s, 64 * 2 ** h, Nf)
+        gf = t["fine"].view(Nf, R).t().cpu()[None, :, :, None]
+        worst = max(worst, (gf - fine).abs().max().item())
+        d, order = torch.cat([d, gf], dim=2).sort(dim=2)
+        if t["fine_sdf"] is not None:
+            sf = o_render.sdf_net(sd, pcfg, c[..., None, :] + v[..., None, :] * gf, False)[0]
+            s = torch.cat([s, sf], 2).gather(2, order)
+    worst = max(worst, (dists_gpu.t().cpu() - d[0, :, :, 0]).abs().max().item())
+    return worst
 
 
 @pytest.mark.parametrize("case", ["hotdog_r64_n32", "hotdog_r64_n128", "pikachu_r32_n192", "savannah_r64_n32"])
@@ -171,16 +202,28 @@ def test_end_to_end_forward_backward(case):
     total_gpu = _gpu_total(out, to_dev(data), pcfg)
     total_gpu.backward()
     g_flat = model.flat.grad.detach().cpu()
-    # oracle
-    sd_o = {k: v.clone().requires_grad_(k.startswith("neural_rgb")) for k, v in fp16_table_sd(sd).items()}
-    o_out = o_render.forward(sd_o, pcfg, data, u=u, training=True, progress=0.0, width=W, height=Hh)
+    # oracle, unconditioned (its own sampler): forward agreement at the PSNR level
+    sd16 = fp16_table_sd(sd)
+    with torch.no_grad():
+        o_free = o_render.forward(sd16, pcfg, data, u=u, training=True, progress=0.0, width=W, height=Hh)
+    for key in ("rgb", "o_r", "o_s", "o_re"):
+        d = (out[key].detach().cpu() - o_free[key]).abs()
+        psnr_d = -10 * math.log10(max(float((d ** 2).mean()), 1e-20))
+        print("%s %s (free) max %.3g mean %.3g psnr(diff) %.1f dB" % (case, key, d.max(), d.mean(), psnr_d))
+        assert d.max() < 0.1 and d.mean() < 2e-3 and psnr_d > 40, key
+    # oracle conditioned on the GPU's sampled dists (sampler checked per round elsewhere):
+    # forward + losses + gradients
+    sd_o = {k: v.clone().requires_grad_(k.startswith("neural_rgb")) for k, v in sd16.items()}
+    o_out = o_render.forward(sd_o, pcfg, data, u=u, training=True, progress=0.0, width=W, height=Hh,
+                             dists=out["dists"].detach().cpu())
     o_total, o_losses, o_psnr = o_render.stage_b_losses(o_out, data, pcfg)
     o_total.backward()
     for key in ("rgb", "o_r", "o_s", "o_re"):
         d = (out[key].detach().cpu() - o_out[key].detach()).abs()
         psnr_d = -10 * math.log10(max(float((d ** 2).mean()), 1e-20))
         print("%s %s max %.3g mean %.3g psnr(diff) %.1f dB" % (case, key, d.max(), d.mean(), psnr_d))
-        assert d.max() < 2e-2 and d.mean() < 2e-3 and psnr_d > 40, key
+        assert d.max() < 2e-2 and d.mean() < 5e-4 and psnr_d > 50, key
+    assert abs(psnr.item() - o_psnr.item()) < 0.1, (psnr.item(), o_psnr.item())
     for k in ("render", "intrinsic", "regularize_re"):
         a, b = losses[k].item(), o_losses[k].item()
         assert abs(a - b) <= 1e-2 * max(abs(b), 1e-3) + 1e-4, (k, a, b)
