@@ -141,15 +141,33 @@ def lib():
     return _lib
 
 
+def _variant(name, args):
+    if name == "mli_sdf":
+        return ":field" if args.mode == 1 else ":sdf"
+    return ""
+
+
 def ptr(t):
     """Device pointer of a tensor (None -> NULL)."""
     return None if t is None else t.data_ptr()
+
+
+# Optional per-launch timing: set to a list to record (name, start_event, end_event) for every
+# C-ABI call on the current stream (used by bench.py for the live roofline measurement).
+PROFILE = None
 
 
 def call(name, args, stream=None):
     import torch
     if stream is None:
         stream = torch.cuda.current_stream().cuda_stream
-    rc = getattr(lib(), name)(C.byref(args), stream)
+    if PROFILE is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rc = getattr(lib(), name)(C.byref(args), stream)
+        e1.record()
+        PROFILE.append((name + _variant(name, args), e0, e1))
+    else:
+        rc = getattr(lib(), name)(C.byref(args), stream)
     if rc != 0:
         raise RuntimeError("%s failed: %s (%d)" % (name, lib().mli_error_string(rc).decode(), rc))
