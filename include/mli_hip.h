@@ -35,7 +35,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mli_stream_t; /* == hipStream_t */
 
-#define MLI_ABI_VERSION 1
+#define MLI_ABI_VERSION 2
 #define MLI_HIDDEN 256
 #define MLI_LEVELS 16
 #define MLI_LEVEL_FEAT 8
@@ -209,19 +209,28 @@ typedef struct {
 int mli_rgb_bwd(const mli_rgb_bwd_args* a, mli_stream_t s);
 
 /* Weight/bias gradients dW_l = dZ_l^T X_l, db_l = sum dZ_l (split-K MFMA GEMM, fp32 atomics
- * into dw/db which the caller zeroes).  Jobs are described in mli_nerf_amd/layout.py. */
+ * into dw/db which the caller zeroes).  Jobs are described in mli_nerf_amd/engine.py.
+ * Jobs fall into three launch classes by shape: BIG (M > 32, K <= 256: 256 x 256 tiles),
+ * WIDE (M > 32, K > 256: 256 x 320 tiles, the 304-wide layer-0 input) and THIN (M <= 32:
+ * 32 x 256); whole-width tiles stream every dZ row once.  `classes` selects which classes
+ * this call launches (bit mask), so a caller can time them separately.  Split-K is sized
+ * per class to fill the 256 CUs. */
 typedef struct {
   const uint16_t* a_rows; /* dZ^T rows [M][S] */
   const uint16_t* b_rows; /* X^T  rows [K][S] */
   int M, K;               /* logical rows of A and B */
-  float* dw;              /* [M][K] fp32 (row stride K) */
+  float* dw;              /* [M][ldw] fp32; this job writes columns [0, K) */
   float* db;              /* [M] fp32 or NULL */
+  int ldw;                /* row stride of dw (>= K) */
 } mli_wgrad_job;
+#define MLI_WGRAD_BIG 1
+#define MLI_WGRAD_WIDE 2
+#define MLI_WGRAD_THIN 4
 typedef struct {
-  int S;
+  int S;                  /* samples (multiple of 64) */
   int n_jobs;
   const mli_wgrad_job* jobs; /* HOST array (copied into the kernel arguments) */
-  int k_split;            /* samples per workgroup (multiple of 64)                          */
+  int classes;            /* MLI_WGRAD_* mask */
 } mli_wgrad_args;
 int mli_wgrad(const mli_wgrad_args* a, mli_stream_t s);
 

@@ -70,11 +70,11 @@ class RgbBwdArgs(C.Structure):
 
 
 class WgradJob(C.Structure):
-    _fields_ = [("a_rows", P), ("b_rows", P), ("M", I32), ("K", I32), ("dw", P), ("db", P)]
+    _fields_ = [("a_rows", P), ("b_rows", P), ("M", I32), ("K", I32), ("dw", P), ("db", P), ("ldw", I32)]
 
 
 class WgradArgs(C.Structure):
-    _fields_ = [("S", I32), ("n_jobs", I32), ("jobs", P), ("k_split", I32)]
+    _fields_ = [("S", I32), ("n_jobs", I32), ("jobs", P), ("classes", I32)]
 
 
 class PackLayer(C.Structure):
@@ -110,6 +110,8 @@ class CastArgs(C.Structure):
     _fields_ = [("src", P), ("dst", P), ("n", I64)]
 
 
+ABI_VERSION = 2  # include/mli_hip.h MLI_ABI_VERSION
+
 ENTRY_POINTS = {
     "mli_rays": RaysArgs, "mli_hashgrid_fwd": HashgridArgs, "mli_sdf": SdfArgs,
     "mli_sample_coarse": SampleCoarseArgs, "mli_sample_fine": SampleFineArgs,
@@ -136,7 +138,7 @@ def lib():
         _lib.mli_abi_version.restype = I32
         _lib.mli_error_string.restype = C.c_char_p
         _lib.mli_error_string.argtypes = [I32]
-        if _lib.mli_abi_version() != 1:
+        if _lib.mli_abi_version() != ABI_VERSION:
             raise ImportError("libmli_hip.so ABI mismatch")
     return _lib
 
@@ -144,6 +146,8 @@ def lib():
 def _variant(name, args):
     if name == "mli_sdf":
         return ":field" if args.mode == 1 else ":sdf"
+    if name == "mli_wgrad":
+        return {1: ":big", 2: ":wide", 4: ":thin"}.get(args.classes, "")
     return ""
 
 

@@ -84,5 +84,11 @@ MLI_FI int opaque_v(int x) {
   asm volatile("" : "+v"(x));
   return x;
 }
+// Per-lane select hi/lo by a 0/~0 mask with integer ops: LLVM folds `c ? a[8+j] : a[j]` into a
+// dynamically indexed load of a private array (scratch); the bitwise form stays in registers.
+MLI_FI float sel_mask(uint32_t mask, float hi, float lo) {
+  const uint32_t r = (__builtin_bit_cast(uint32_t, hi) & mask) | (__builtin_bit_cast(uint32_t, lo) & ~mask);
+  return __builtin_bit_cast(float, r);
+}
 
 #define MLI_LAUNCH_CHECK() return (int)hipGetLastError()

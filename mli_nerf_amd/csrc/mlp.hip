@@ -26,6 +26,11 @@ constexpr int WAVES = 8;
 constexpr int BUF = 20480;  // >= 19 KiB + 128 B (largest chunk), multiple of 256
 constexpr int CH(int ks) { return ks * 1024 + 128; }
 constexpr int FRAG_TILE = 16 * 64 * 8;  // halves per 32-sample tile of a 256-wide frag image
+// Feature-major activation tiles ([32 features][256 samples] fp16 per n-tile per workgroup)
+// are transposed through LDS so each row leaves as 512 contiguous bytes in 16 B stores.
+constexpr int SROW = 256 * 2 + 16;       // staged row stride (16 B pad)
+constexpr int STAGE = 32 * SROW;
+constexpr int LDS_BYTES = 2 * BUF + 2 * STAGE;
 
 struct Pipe {
   const uint8_t* next;
@@ -62,6 +67,41 @@ MLI_FI void pipe_start(Pipe& p, uint8_t* lds, int bytes) {
   __syncthreads();
 }
 
+// Double-buffered LDS staging of feature-major tiles: stage_tile() writes a tile (the
+// accumulator layout: rows acc_row(i, h), sample column wave*32 + c) into one buffer; the
+// next workgroup barrier (inside run_layer) makes it visible and stage_flush() writes it
+// out while the other buffer takes the next tile.
+struct Stager {
+  uint16_t* pend;  // global address of (row 0, first sample of the block) of the staged tile
+  int buf, pbuf;
+};
+
+MLI_FI void stage_tile(Stager& sg, uint8_t* lds, const f32x16& v, uint16_t* dst, int lane) {
+  const int wave = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
+  uint8_t* sb = lds + 2 * BUF + sg.buf * STAGE + (4 * h) * SROW + (wave * 32 + c) * 2;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const f16 x = (f16)v[i];
+    *reinterpret_cast<uint16_t*>(sb + ((i & 3) + 8 * (i >> 2)) * SROW) = __builtin_bit_cast(uint16_t, x);
+  }
+  sg.pend = dst;
+  sg.pbuf = sg.buf;
+  sg.buf ^= 1;
+}
+
+MLI_FI void stage_flush(Stager& sg, const uint8_t* lds, int S) {
+  if (sg.pend == nullptr) return;
+  const int row = threadIdx.x >> 5, col = threadIdx.x & 31;
+  const uint8_t* sb = lds + 2 * BUF + sg.pbuf * STAGE;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int r = row + 16 * u;
+    const u32x4 x = *reinterpret_cast<const u32x4*>(sb + r * SROW + col * 16);
+    *reinterpret_cast<u32x4*>(sg.pend + (size_t)r * S + col * 8) = x;
+  }
+  sg.pend = nullptr;
+}
+
 // acc = W_chunk (32 x 16*KS) * X (16*KS x 32) + bias
 template <int KS>
 MLI_FI f32x16 chunk_mma(const uint8_t* chunk, const half8* X, int lane) {
@@ -76,13 +116,23 @@ MLI_FI f32x16 chunk_mma(const uint8_t* chunk, const half8* X, int lane) {
   const half8* w = reinterpret_cast<const half8*>(chunk) + lane;
 #pragma unroll
   for (int q = 0; q < KS; ++q) acc = mfma32(w[q * 64], X[q], acc);
+  // keep at most RA weight fragments in flight (register pressure): RA reads, then one
+  // read per MFMA
+  constexpr int RA = KS < 4 ? KS : 4;
+  __builtin_amdgcn_sched_group_barrier(0x100, RA, 0);
+#pragma unroll
+  for (int q = 0; q < KS; ++q) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    if (q + RA < KS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+  }
   return acc;
 }
 
 // One layer of NT n-tiles over KS k-steps; `next_bytes` = size of the chunk after this layer.
 // epi(t, acc) consumes each finished tile.
 template <int KS, int NT, class Epi>
-MLI_FI void run_layer(Pipe& p, uint8_t* lds, const half8* X, int lane, int next_bytes, Epi&& epi) {
+MLI_FI void run_layer(Pipe& p, uint8_t* lds, Stager& sg, int S, const half8* X, int lane, int next_bytes,
+                      Epi&& epi) {
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int nb = (t + 1 < NT) ? CH(KS) : next_bytes;
@@ -91,18 +141,8 @@ MLI_FI void run_layer(Pipe& p, uint8_t* lds, const half8* X, int lane, int next_
     if (nb) pipe_commit(p, lds);
     __syncthreads();
     p.buf ^= 1;
+    stage_flush(sg, lds, S);
     epi(t, acc);
-  }
-}
-
-MLI_FI void store_fm(uint16_t* base, int S, int t, int h, int m, const f32x16& v) {
-  // feature-major [256][S] fp16 store of one accumulator tile (feature rows of tile t):
-  // one per-lane offset (rows 32t+4h, column m) + a scalar row offset per register.
-  uint16_t* lane_base = base + ((uint32_t)(32 * t + 4 * h) * (uint32_t)S + (uint32_t)m);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const uint32_t roff = (uint32_t)((i & 3) + 8 * (i >> 2)) * (uint32_t)S;
-    lane_base[roff] = __builtin_bit_cast(uint16_t, (f16)v[i]);
   }
 }
 
@@ -143,20 +183,17 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
     sh16(a.pts_light[3 * r], a.pts_light[3 * r + 1], a.pts_light[3 * r + 2], shl);
     sh16(vr[0], vr[1], vr[2], shv);
     const float e16[8] = {p[0], p[1], p[2], nrm[0], nrm[1], nrm[2], 0.f, 0.f};
+    const uint32_t hm = opaque_v(h) ? ~0u : 0u;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float l_lo = shl[j], l_hi = shl[8 + j], v_lo = shv[j], v_hi = shv[8 + j];
-      B[16][j] = (f16)(h ? 0.f : e16[j]);
-      B[17][j] = (f16)(h ? l_hi : l_lo);
-      B[18][j] = (f16)(h ? v_hi : v_lo);
-    }
-    if (train) {
-      // feature-major rows 256..303 (k_nat order) from the fp32 sources
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float v16 = h ? 0.f : e16[j];
-        const float v17 = h ? shl[8 + j] : shl[j];
-        const float v18 = h ? shv[8 + j] : shv[j];
+      const float v16 = sel_mask(hm, 0.f, e16[j]);
+      const float v17 = sel_mask(hm, shl[8 + j], shl[j]);
+      const float v18 = sel_mask(hm, shv[8 + j], shv[j]);
+      B[16][j] = (f16)v16;
+      B[17][j] = (f16)v17;
+      B[18][j] = (f16)v18;
+      if (train) {
+        // feature-major rows 256..303 (k_nat order) from the fp32 sources
         a.x0T[(size_t)k_nat(16, h, j) * S + m] = __builtin_bit_cast(uint16_t, (f16)v16);
         a.x0T[(size_t)k_nat(17, h, j) * S + m] = __builtin_bit_cast(uint16_t, (f16)v17);
         a.x0T[(size_t)k_nat(18, h, j) * S + m] = __builtin_bit_cast(uint16_t, (f16)v18);
@@ -167,10 +204,12 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
   Pipe pipe;
   pipe.next = reinterpret_cast<const uint8_t*>(a.wfwd);
   pipe_start(pipe, lds, CH(16));
+  Stager sg{nullptr, 0, 0};
+  const size_t col0 = (size_t)blockIdx.x * 256;
 
   // SDF layer 1: feat = softplus(W1 h0 + b1) -> A; frag image scratch (+ x0T rows 0..255)
   uint16_t* ftile = a.feat_frag + (size_t)tile * FRAG_TILE;
-  run_layer<16, 8>(pipe, lds, B, lane, CH(19), [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
+  run_layer<16, 8>(pipe, lds, sg, S, B, lane, CH(19), [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
     f32x16 v;
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = softplus100(acc[i]);
@@ -179,14 +218,15 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
     half8* dst = reinterpret_cast<half8*>(ftile) + (2 * t) * 64 + lane;
     dst[0] = A[2 * t];
     dst[64] = A[2 * t + 1];
-    if (train) store_fm(a.x0T, S, t, h, m, v);
+    if (train) stage_tile(sg, lds, v, a.x0T + (size_t)(32 * t) * S + col0, lane);
   });
 
   for (int hd = 0; hd < 3; ++hd) {
     const int S = opaque_s(a.R * a.N);
-    // reload feat frags into B[0..15] (B[16..18] keep the extras)
+    // reload feat frags into B[0..15] (B[16..18] keep the extras); the lane offset is made
+    // opaque per head so the 16 addresses are not hoisted out of the head loop (spills)
     {
-      const half8* src = reinterpret_cast<const half8*>(ftile) + lane;
+      const half8* src = reinterpret_cast<const half8*>(ftile) + opaque_v(lane);
 #pragma unroll
       for (int q = 0; q < 16; ++q) B[q] = src[q * 64];
     }
@@ -203,7 +243,7 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
 #pragma unroll
           for (int i = 0; i < 16; ++i) bits |= (acc[i] > 0.0f ? 1u : 0u) << i;
           if (t & 1) mbits[t >> 1] |= bits << 16; else mbits[t >> 1] = bits;
-          store_fm(a.xT + ((size_t)(hd * 4 + layer) * 256) * S, S, t, h, m, v);
+          stage_tile(sg, lds, v, a.xT + ((size_t)(hd * 4 + layer) * 256 + 32 * t) * S + col0, lane);
           if (t == 7) {
             u32x4* mp = reinterpret_cast<u32x4*>(a.masks) +
                         ((size_t)(hd * 4 + layer) * (S / 32) + tile) * 64 + lane;
@@ -212,14 +252,14 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
         }
       };
     };
-    run_layer<19, 8>(pipe, lds, B, lane, CH(16), relu_epi(A, 0));
-    run_layer<16, 8>(pipe, lds, A, lane, CH(16), relu_epi(B, 1));
-    run_layer<16, 8>(pipe, lds, B, lane, CH(16), relu_epi(A, 2));
-    run_layer<16, 8>(pipe, lds, A, lane, CH(16), relu_epi(B, 3));
+    run_layer<19, 8>(pipe, lds, sg, S, B, lane, CH(16), relu_epi(A, 0));
+    run_layer<16, 8>(pipe, lds, sg, S, A, lane, CH(16), relu_epi(B, 1));
+    run_layer<16, 8>(pipe, lds, sg, S, B, lane, CH(16), relu_epi(A, 2));
+    run_layer<16, 8>(pipe, lds, sg, S, A, lane, CH(16), relu_epi(B, 3));
     const int after = (hd < 2) ? CH(19) : 0;
     const int no = hd == 2 ? 1 : 3;
     const int off = hd * 3;
-    run_layer<16, 1>(pipe, lds, B, lane, after, [&](int, const f32x16& acc) MLI_LAMBDA_FI {
+    run_layer<16, 1>(pipe, lds, sg, S, B, lane, after, [&](int, const f32x16& acc) MLI_LAMBDA_FI {
       if (h == 0) {
 #pragma unroll
         for (int i = 0; i < 3; ++i)
@@ -245,6 +285,8 @@ __global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
   Pipe pipe;
   pipe.next = reinterpret_cast<const uint8_t*>(a.wbwd);
   pipe_start(pipe, lds, CH(1));
+  Stager sg{nullptr, 0, 0};
+  const size_t col0 = (size_t)blockIdx.x * 256;
   for (int hd = 0; hd < 3; ++hd) {
     const int S = opaque_s(a.R * a.N);
     const int no = hd == 2 ? 1 : 3;
@@ -274,14 +316,16 @@ __global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
         for (int i = 0; i < 16; ++i) v[i] = ((bits >> i) & 1u) ? acc[i] : 0.0f;
         out[2 * t] = acc_to_frag(v, 0);
         out[2 * t + 1] = acc_to_frag(v, 1);
-        store_fm(a.dzT + ((size_t)(hd * 4 + layer) * 256) * S, S, t, h, m, v);
+        stage_tile(sg, lds, v, a.dzT + ((size_t)(hd * 4 + layer) * 256 + 32 * t) * S + col0, lane);
       };
     };
-    run_layer<1, 8>(pipe, lds, &z4, lane, CH(16), mask_epi(A, 3, 3));
-    run_layer<16, 8>(pipe, lds, A, lane, CH(16), mask_epi(B, 2, 2));
-    run_layer<16, 8>(pipe, lds, B, lane, CH(16), mask_epi(A, 1, 1));
-    run_layer<16, 8>(pipe, lds, A, lane, hd < 2 ? CH(1) : 0, mask_epi(B, 0, 0));
+    run_layer<1, 8>(pipe, lds, sg, S, &z4, lane, CH(16), mask_epi(A, 3, 3));
+    run_layer<16, 8>(pipe, lds, sg, S, A, lane, CH(16), mask_epi(B, 2, 2));
+    run_layer<16, 8>(pipe, lds, sg, S, B, lane, CH(16), mask_epi(A, 1, 1));
+    run_layer<16, 8>(pipe, lds, sg, S, A, lane, hd < 2 ? CH(1) : 0, mask_epi(B, 0, 0));
   }
+  __syncthreads();
+  stage_flush(sg, lds, opaque_s(a.R * a.N));
 }
 
 }  // namespace
@@ -289,13 +333,13 @@ __global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
 extern "C" int mli_rgb_fwd(const mli_rgb_fwd_args* a, mli_stream_t s) {
   const int S = a->R * a->N;
   if (S % 256 != 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(rgb_fwd_kernel, dim3(S / 256), dim3(THREADS), 2 * BUF, (hipStream_t)s, *a);
+  hipLaunchKernelGGL(rgb_fwd_kernel, dim3(S / 256), dim3(THREADS), LDS_BYTES, (hipStream_t)s, *a);
   MLI_LAUNCH_CHECK();
 }
 
 extern "C" int mli_rgb_bwd(const mli_rgb_bwd_args* a, mli_stream_t s) {
   const int S = a->R * a->N;
   if (S % 256 != 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(rgb_bwd_kernel, dim3(S / 256), dim3(THREADS), 2 * BUF, (hipStream_t)s, *a);
+  hipLaunchKernelGGL(rgb_bwd_kernel, dim3(S / 256), dim3(THREADS), LDS_BYTES, (hipStream_t)s, *a);
   MLI_LAUNCH_CHECK();
 }

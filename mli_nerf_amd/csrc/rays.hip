@@ -99,77 +99,168 @@ MLI_FI float section_alpha(float d0, float d1, float s0, float s1, float& prev_c
   return fminf(fmaxf(al, 0.0f), 1.0f);
 }
 
-// One thread per ray: merge the two sorted lists (torch.sort of cat, ties irrelevant:
-// equal dists are the same point, hence the same sdf), then draw Nf fine dists by the
-// section pdf's inverse CDF (nerf_util.py:41-68), walking the cdf once.
-__global__ __launch_bounds__(128) void sample_fine_kernel(FineArgs fa) {
+// Wave-level scans over 64 lanes (Hillis-Steele through ds_bpermute).
+MLI_FI float wave_excl_prod(float x, int lane) {
+  float v = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float y = __shfl_up(v, o);
+    if (lane >= o) v *= y;
+  }
+  const float e = __shfl_up(v, 1);
+  return lane == 0 ? 1.0f : e;
+}
+MLI_FI float wave_excl_sum(float x, int lane) {
+  float v = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float y = __shfl_up(v, o);
+    if (lane >= o) v += y;
+  }
+  const float e = __shfl_up(v, 1);
+  return lane == 0 ? 0.0f : e;
+}
+MLI_FI float wave_sum(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
+// One wave per ray (FW rays per block), the ray's lists staged in LDS:
+//  1. merge = torch.sort(cat(a, b)) (neuralangelo/model.py:461): every element's output
+//     slot is its rank under (dist, list a first, index) -- a upper-bound binary search in
+//     the sorted list a for b's elements, a linear count over b (<= 64) for a's -- so the
+//     scatter is a permutation even if b is not exactly sorted;
+//  2. section alphas (robust cos, model.py:467-482), exclusive transmittance
+//     (render.py:87-99) and the L1-normalised pdf / cdf (nerf_util.py:41-57) by wave scans,
+//     each lane owning 4 consecutive sections;
+//  3. inverse CDF at the midpoint quantiles: searchsorted(cdf, u, right) by binary search
+//     (nerf_util.py:58-68), one lane per fine sample.
+constexpr int FW = 4;
+constexpr int FMAX = 256;  // Na + Nb
+constexpr int FBMAX = 64;  // Nb, Nf
+__global__ __launch_bounds__(FW * 64) void sample_fine_kernel(FineArgs fa) {
   const mli_sample_fine_args& a = fa.a;
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= a.R) return;
-  const int R = a.R;
-  const int Nh = a.Na + a.Nb;
-  {
-    int i = 0, j = 0;
-    for (int o = 0; o < Nh; ++o) {
-      const float da = i < a.Na ? a.dists_a[(size_t)i * R + r] : INFINITY;
-      const float db = j < a.Nb ? a.dists_b[(size_t)j * R + r] : INFINITY;
-      const bool take_a = (j >= a.Nb) || (i < a.Na && da <= db);
-      float dv, sv = 0.f;
-      if (take_a) {
-        dv = da;
-        if (a.sdf_out) sv = a.sdf_a[(size_t)i * R + r];
-        ++i;
-      } else {
-        dv = db;
-        if (a.sdf_out) sv = a.sdf_b[(size_t)j * R + r];
-        ++j;
-      }
-      a.dists_out[(size_t)o * R + r] = dv;
-      if (a.sdf_out) a.sdf_out[(size_t)o * R + r] = sv;
+  __shared__ float s_ad[FW][FMAX], s_bd[FW][FBMAX], s_md[FW][FMAX], s_ms[FW][FMAX], s_cd[FW][FMAX];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int R = a.R, Na = a.Na, Nb = a.Nb, Nh = Na + Nb;
+  const int r = min((int)(blockIdx.x * FW + w), R - 1);  // tail waves redo the last ray (same values)
+  float* ad = s_ad[w];
+  float* bd = s_bd[w];
+  float* md = s_md[w];
+  float* ms = s_ms[w];
+  float* cd = s_cd[w];
+  const bool with_sdf = a.sdf_out != nullptr;
+  // ---- 1. merge
+  float av[FMAX / 64], as[FMAX / 64];
+#pragma unroll
+  for (int e = 0; e < FMAX / 64; ++e) {
+    const int i = lane + 64 * e;
+    av[e] = i < Na ? a.dists_a[(size_t)i * R + r] : 0.f;
+    as[e] = (i < Na && with_sdf) ? a.sdf_a[(size_t)i * R + r] : 0.f;
+    if (i < Na) ad[i] = av[e];
+  }
+  const float bv = lane < Nb ? a.dists_b[(size_t)lane * R + r] : 0.f;
+  const float bs = (lane < Nb && with_sdf) ? a.sdf_b[(size_t)lane * R + r] : 0.f;
+  if (lane < Nb) bd[lane] = bv;
+  __syncthreads();
+  int apos[FMAX / 64];
+#pragma unroll
+  for (int e = 0; e < FMAX / 64; ++e) apos[e] = lane + 64 * e;
+  int bpos = 0;
+  for (int j = 0; j < Nb; ++j) {
+    const float y = bd[j];
+#pragma unroll
+    for (int e = 0; e < FMAX / 64; ++e) apos[e] += (y < av[e]) ? 1 : 0;
+    bpos += (y < bv || (y == bv && j < lane)) ? 1 : 0;
+  }
+  if (lane < Nb) {  // + #{i : a_i <= bv}
+    int lo = 0, hi = Na;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (ad[mid] <= bv) lo = mid + 1; else hi = mid;
+    }
+    bpos += lo;
+  }
+  const bool store = blockIdx.x * FW + w < R;
+#pragma unroll
+  for (int e = 0; e < FMAX / 64; ++e) {
+    if (lane + 64 * e < Na) {
+      md[apos[e]] = av[e];
+      ms[apos[e]] = as[e];
+    }
+  }
+  if (lane < Nb) {
+    md[bpos] = bv;
+    ms[bpos] = bs;
+  }
+  __syncthreads();
+  for (int i = lane; i < Nh; i += 64) {
+    if (store) {
+      a.dists_out[(size_t)i * R + r] = md[i];
+      if (with_sdf) a.sdf_out[(size_t)i * R + r] = ms[i];
     }
   }
   if (a.Nf == 0) return;
-  const float* D = a.dists_out;
-  const float* S = a.sdf_out;
-  // pass 1: L1 norm of the section weights (F.normalize p=1, eps 1e-12)
-  float l1 = 0.f;
+  // ---- 2. sections i = 4*lane + e (i + 1 < Nh)
+  constexpr int E = FMAX / 64;
+  float al[E], q[E];
   {
-    float T = 1.f, pc = 0.f;
-    float d0 = D[r], s0 = S[r];
-    for (int i = 0; i + 1 < Nh; ++i) {
-      const float d1 = D[(size_t)(i + 1) * R + r], s1 = S[(size_t)(i + 1) * R + r];
-      const float al = section_alpha(d0, d1, s0, s1, pc, a.inv_s);
-      l1 += fabsf(al * T);
-      T = T * (1.0f - al);
-      d0 = d1; s0 = s1;
+    const int i0 = E * lane;
+    float prev_raw = 0.f;
+    if (i0 >= 1 && i0 < Nh) {
+      const float dm = md[i0 - 1], sm = ms[i0 - 1];
+      prev_raw = (ms[i0] - sm) / ((md[i0] - dm) + 1e-5f);
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = i0 + e;
+      al[e] = 0.f;
+      if (i + 1 < Nh) {
+        float pc = prev_raw;
+        al[e] = section_alpha(md[i], md[i + 1], ms[i], ms[i + 1], pc, a.inv_s);
+        prev_raw = pc;
+      }
+      q[e] = 1.0f - al[e];
     }
   }
-  const float den = fmaxf(l1, 1e-12f);
-  // pass 2: cdf walk; idx_j = #{k : cdf_k <= u_j} (searchsorted right)
-  int j = 0;
-  float T = 1.f, pc = 0.f, cdf = 0.f;
-  float d0 = D[r], s0 = S[r];
-  float cprev = 0.f, dprev = d0;
-  // k = 0: cdf_0 = 0 (never > u)
-  for (int i = 0; i + 1 < Nh && j < a.Nf; ++i) {
-    const float d1 = D[(size_t)(i + 1) * R + r], s1 = S[(size_t)(i + 1) * R + r];
-    const float al = section_alpha(d0, d1, s0, s1, pc, a.inv_s);
-    const float pdf = (al * T) / den;
-    T = T * (1.0f - al);
-    cprev = cdf;
-    dprev = d0;
-    cdf = cdf + pdf;  // cdf_{i+1}
-    while (j < a.Nf && cdf > fa.u[j]) {  // idx = i+1: low = i, high = i+1
-      const float u = fa.u[j];
-      const float t = (u - cprev) / ((cdf - cprev) + 1e-8f);
-      a.fine_out[(size_t)j * R + r] = dprev + t * (d1 - dprev);
-      ++j;
-    }
-    d0 = d1; s0 = s1;
+  float lp = 1.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e) lp *= q[e];
+  float T = wave_excl_prod(lp, lane);
+  float wv[E], l1 = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    wv[e] = al[e] * T;
+    T = T * q[e];
+    l1 += fabsf(wv[e]);
   }
-  // idx = Nh: low = high = Nh-1 -> the last dist
-  const float dl = D[(size_t)(Nh - 1) * R + r];
-  for (; j < a.Nf; ++j) a.fine_out[(size_t)j * R + r] = dl + ((fa.u[j] - cdf) / (0.f + 1e-8f)) * (dl - dl);
+  const float den = fmaxf(wave_sum(l1), 1e-12f);
+  float c[E], run = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    run += wv[e] / den;
+    c[e] = run;
+  }
+  const float base = wave_excl_sum(run, lane);
+  if (lane == 0) cd[0] = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e)
+    if (E * lane + e + 1 < Nh) cd[E * lane + e + 1] = base + c[e];
+  __syncthreads();
+  // ---- 3. inverse CDF, lane j -> fine sample j
+  if (lane < a.Nf && store) {
+    const float u = fa.u[lane];
+    int lo = 0, hi = Nh;  // idx = #{k : cdf_k <= u}
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (cd[mid] <= u) lo = mid + 1; else hi = mid;
+    }
+    const int i_lo = max(lo - 1, 0), i_hi = min(lo, Nh - 1);
+    const float d0 = md[i_lo], d1 = md[i_hi], c0 = cd[i_lo], c1 = cd[i_hi];
+    const float t = (u - c0) / ((c1 - c0) + 1e-8f);
+    a.fine_out[(size_t)lane * R + r] = d0 + t * (d1 - d0);
+  }
 }
 
 // --------------------------------------------------------------------------- composite
@@ -277,12 +368,12 @@ extern "C" int mli_sample_coarse(const mli_sample_coarse_args* a, mli_stream_t s
 
 extern "C" int mli_sample_fine(const mli_sample_fine_args* a, mli_stream_t s) {
   if (a->R <= 0) return 0;
-  if (a->Nf > 64) return (int)hipErrorInvalidValue;
+  if (a->Nf > FBMAX || a->Nb > FBMAX || a->Na < 1 || a->Na + a->Nb > FMAX) return (int)hipErrorInvalidValue;
   if (a->Nf > 0 && a->sdf_out == nullptr) return (int)hipErrorInvalidValue;
   FineArgs fa;
   fa.a = *a;
   for (int j = 0; j < 64; ++j) fa.u[j] = (j < a->Nf && a->u_fine) ? a->u_fine[j] : 2.0f;
-  hipLaunchKernelGGL(sample_fine_kernel, dim3((a->R + 127) / 128), dim3(128), 0, (hipStream_t)s, fa);
+  hipLaunchKernelGGL(sample_fine_kernel, dim3((a->R + FW - 1) / FW), dim3(FW * 64), 0, (hipStream_t)s, fa);
   MLI_LAUNCH_CHECK();
 }
 

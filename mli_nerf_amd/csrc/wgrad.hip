@@ -8,6 +8,8 @@
 // output element per slice).
 #include "common.h"
 
+#include <algorithm>
+
 namespace {
 
 constexpr int MAXJOBS = 16;
@@ -16,7 +18,7 @@ constexpr int ROWB = BK * 2 + 16;      // LDS row stride in bytes (16 B pad: con
 
 struct Job {
   const uint16_t* a; const uint16_t* b;
-  int M, K;
+  int M, K, ldw;
   float* dw; float* db;
   int tiles_n, tile_base;
 };
@@ -128,7 +130,7 @@ __global__ __launch_bounds__(512) void wgrad_kernel(KArgs ka) {
       for (int e = 0; e < 16; ++e) {
         const int row = tm * BM + wm * TM * 32 + i * 32 + acc_row(e, h);
         const int col = tn * BN + wn * TN * 32 + j * 32 + rl;
-        if (row < J.M && col < J.K) atomicAdd(J.dw + (size_t)row * J.K + col, acc[i][j][e]);
+        if (row < J.M && col < J.K) atomicAdd(J.dw + (size_t)row * J.ldw + col, acc[i][j][e]);
       }
   if (do_bias) {
     bsum += __shfl_xor(bsum, 1);
@@ -137,25 +139,39 @@ __global__ __launch_bounds__(512) void wgrad_kernel(KArgs ka) {
   }
 }
 
-template <int BM, int BN, int WM, int WN>
-int launch(const mli_wgrad_args* a, bool thin, hipStream_t s) {
+enum { CLS_BIG = 1, CLS_WIDE = 2, CLS_THIN = 4 };
+
+inline int job_class(const mli_wgrad_job& j) {
+  return j.M <= 32 ? CLS_THIN : (j.K <= 256 ? CLS_BIG : CLS_WIDE);
+}
+
+// One launch per class: tiles of all its jobs x n_split k-slices, n_split sized so the
+// grid holds about OCC workgroups per CU (OCC = resident 512-thread workgroups per CU).
+template <int BM, int BN, int WM, int WN, int OCC>
+int launch(const mli_wgrad_args* a, int cls, hipStream_t s) {
   KArgs ka;
   ka.S = a->S;
-  ka.k_split = a->k_split;
-  ka.n_split = (a->S + a->k_split - 1) / a->k_split;
-  int n = 0, base = 0;
+  int n = 0, tiles = 0;
   for (int i = 0; i < a->n_jobs; ++i) {
     const mli_wgrad_job& j = a->jobs[i];
-    if ((j.M <= 32) != thin) continue;
-    if (n == MAXJOBS) return (int)hipErrorInvalidValue;
+    if (job_class(j) != cls) continue;
+    if (n == MAXJOBS || j.ldw < j.K || j.M <= 0 || j.K <= 0) return (int)hipErrorInvalidValue;
     Job& J = ka.jobs[n++];
-    J.a = j.a_rows; J.b = j.b_rows; J.M = j.M; J.K = j.K; J.dw = j.dw; J.db = j.db;
+    J.a = j.a_rows; J.b = j.b_rows; J.M = j.M; J.K = j.K; J.ldw = j.ldw; J.dw = j.dw; J.db = j.db;
     J.tiles_n = (j.K + BN - 1) / BN;
-    J.tile_base = base;
-    base += ((j.M + BM - 1) / BM) * J.tiles_n * ka.n_split;
+    tiles += ((j.M + BM - 1) / BM) * J.tiles_n;
   }
   ka.n_jobs = n;
   if (n == 0) return 0;
+  const int want = std::max(1, 256 * OCC / tiles);
+  const int steps = a->S / BK;
+  ka.k_split = ((steps + want - 1) / want) * BK;
+  ka.n_split = (a->S + ka.k_split - 1) / ka.k_split;
+  int base = 0;
+  for (int i = 0; i < n; ++i) {
+    ka.jobs[i].tile_base = base;
+    base += ((ka.jobs[i].M + BM - 1) / BM) * ka.jobs[i].tiles_n * ka.n_split;
+  }
   hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN>), dim3(base), dim3(512), (BM + BN) * ROWB, s, ka);
   return (int)hipGetLastError();
 }
@@ -163,8 +179,10 @@ int launch(const mli_wgrad_args* a, bool thin, hipStream_t s) {
 }  // namespace
 
 extern "C" int mli_wgrad(const mli_wgrad_args* a, mli_stream_t s) {
-  if (a->S % BK != 0 || a->k_split % BK != 0) return (int)hipErrorInvalidValue;
-  int e = launch<256, 128, 4, 2>(a, false, (hipStream_t)s);
-  if (e) return e;
-  return launch<32, 256, 1, 8>(a, true, (hipStream_t)s);
+  if (a->S <= 0 || a->S % BK != 0) return (int)hipErrorInvalidValue;
+  int e = 0;
+  if (a->classes & CLS_BIG) e = launch<256, 256, 4, 2, 1>(a, CLS_BIG, (hipStream_t)s);
+  if (!e && (a->classes & CLS_WIDE)) e = launch<256, 320, 4, 2, 1>(a, CLS_WIDE, (hipStream_t)s);
+  if (!e && (a->classes & CLS_THIN)) e = launch<32, 256, 1, 8, 2>(a, CLS_THIN, (hipStream_t)s);
+  return e;
 }

@@ -252,6 +252,53 @@ class RenderEngine:
         return rays, dists, fld, hd, comp
 
     # ------------------------------------------------------------------ backward
+    @staticmethod
+    def _dw_sizes():
+        sizes = []
+        for name, k_in, k_out in layout.HEADS:
+            sizes += [(256, layout.K0), (256, 256), (256, 256), (256, 256), (k_out, 256)]
+        return sizes
+
+    def _dw_total(self):
+        return sum(m * k + m for m, k in self._dw_sizes())
+
+    def _wgrad_plan(self, dzT, dz4T, hd, dwbuf, flat, grad_out, S):
+        """Split-K jobs (host array) + device assemble descriptors; cached per buffer set."""
+        key = (dzT.data_ptr(), dz4T.data_ptr(), hd["x0T"].data_ptr(), hd["xT"].data_ptr(), dwbuf.data_ptr(),
+               flat.data_ptr(), grad_out.data_ptr(), S)
+        if getattr(self, "_wplan", None) is not None and self._wplan[0] == key:
+            return self._wplan[1], self._wplan[2]
+        sizes = self._dw_sizes()
+        jobs, assemble, keep, off = [], [], [], 0
+        for hdx, (name, k_in, k_out) in enumerate(layout.HEADS):
+            for li in range(5):
+                m, k = sizes[hdx * 5 + li]
+                dw = dwbuf[off:off + m * k]
+                db = dwbuf[off + m * k:off + m * k + m]
+                off += m * k + m
+                if li == 0:
+                    a_rows, b_rows = dzT[hdx, 0], hd["x0T"]
+                elif li < 4:
+                    a_rows, b_rows = dzT[hdx, li], hd["xT"][hdx, li - 1]
+                else:
+                    a_rows, b_rows = dz4T[hdx], hd["xT"][hdx, 3]
+                jobs.append(L.WgradJob(L.ptr(a_rows), L.ptr(b_rows), m, k, L.ptr(dw), L.ptr(db), k))
+                pre = layout.param_prefix(name, li)
+                v = self.param_view(flat, pre + ".weight_v")
+                g = self.param_view(flat, pre + ".weight_g")
+                k_ref = v.shape[1]
+                kinv = layout.head_kinv(name, k_ref) if li == 0 else np.arange(k_ref, dtype=np.int16)
+                kinv_t = torch.from_numpy(kinv.astype(np.int16)).to(self.device)
+                keep.append(kinv_t)
+                assemble.append(L.AssembleLayer(L.ptr(dw), L.ptr(db), L.ptr(v), L.ptr(g), m, k_ref, k,
+                                                L.ptr(kinv_t), L.ptr(self.param_view(grad_out, pre + ".weight_v")),
+                                                L.ptr(self.param_view(grad_out, pre + ".weight_g")),
+                                                L.ptr(self.param_view(grad_out, pre + ".bias")), None))
+        job_arr = (L.WgradJob * len(jobs))(*jobs)
+        ad = _to_device_structs(assemble, self.device)
+        self._wplan = (key, job_arr, ad, keep)
+        return job_arr, ad
+
     @torch.no_grad()
     def backward(self, st, d_rgb, d_o_r, d_o_s, d_o_re, flat, sdf_l1, grad_out):
         """Gradient of the loss w.r.t. the trainable head parameters into grad_out (flat)."""
@@ -270,44 +317,12 @@ class RenderEngine:
         L.call("mli_rgb_bwd", L.RgbBwdArgs(R, N, L.ptr(dz4), L.ptr(self.wbwd), L.ptr(hd["masks"]), L.ptr(dzT),
                                            L.ptr(dz4T)))
         # weight gradients (packed-k space), zeroed then accumulated by split-K atomics
-        sizes = []
-        for hdx, (name, k_in, k_out) in enumerate(layout.HEADS):
-            sizes += [(256, layout.K0), (256, 256), (256, 256), (256, 256), (k_out, 256)]
-        total = sum(m * k + m for m, k in sizes)
-        dwbuf = self._buf("dw", (total,))
+        dwbuf = self._buf("dw", (self._dw_total(),))
         dwbuf.zero_()
-        jobs, assemble, off = [], [], 0
-        self._kinv_keep = []
-        for hdx, (name, k_in, k_out) in enumerate(layout.HEADS):
-            for li in range(5):
-                m, k = sizes[hdx * 5 + li]
-                dw = dwbuf[off:off + m * k]
-                db = dwbuf[off + m * k:off + m * k + m]
-                off += m * k + m
-                if li == 0:
-                    a_rows, b_rows = dzT[hdx, 0], hd["x0T"]
-                elif li < 4:
-                    a_rows, b_rows = dzT[hdx, li], hd["xT"][hdx, li - 1]
-                else:
-                    a_rows, b_rows = dz4T[hdx], hd["xT"][hdx, 3]
-                jobs.append(L.WgradJob(L.ptr(a_rows), L.ptr(b_rows), m, k, L.ptr(dw), L.ptr(db)))
-                pre = layout.param_prefix(name, li)
-                v = self.param_view(flat, pre + ".weight_v")
-                g = self.param_view(flat, pre + ".weight_g")
-                k_ref = v.shape[1]
-                kinv = layout.head_kinv(name, k_ref) if li == 0 else np.arange(k_ref, dtype=np.int16)
-                kinv_t = torch.from_numpy(kinv.astype(np.int16)).to(self.device)
-                self._kinv_keep.append(kinv_t)
-                assemble.append(L.AssembleLayer(L.ptr(dw), L.ptr(db), L.ptr(v), L.ptr(g), m, k_ref, k,
-                                                L.ptr(kinv_t), L.ptr(self.param_view(grad_out, pre + ".weight_v")),
-                                                L.ptr(self.param_view(grad_out, pre + ".weight_g")),
-                                                L.ptr(self.param_view(grad_out, pre + ".bias")), None))
-        job_arr = (L.WgradJob * len(jobs))(*jobs)
-        k_split = 32768 if S >= 32768 * 4 else max(64, (S // 4) // 64 * 64)
-        L.call("mli_wgrad", L.WgradArgs(S, len(jobs), C.cast(job_arr, C.c_void_p), k_split))
-        ad = _to_device_structs(assemble, self.device)
-        self._assemble_keep = ad
-        L.call("mli_grad_assemble", L.AssembleArgs(len(assemble), L.ptr(ad), 1.0 / scale))
+        jobs, ad = self._wgrad_plan(dzT, dz4T, hd, dwbuf, flat, grad_out, S)
+        for cls in (1, 2, 4):  # BIG, WIDE, THIN launch classes (timed separately)
+            L.call("mli_wgrad", L.WgradArgs(S, len(jobs), C.cast(jobs, C.c_void_p), cls))
+        L.call("mli_grad_assemble", L.AssembleArgs(15, L.ptr(ad), 1.0 / scale))
         return grad_out
 
 

@@ -1,0 +1,77 @@
+"""C-ABI boundary checks that need no GPU: the ctypes mirrors in mli_nerf_amd/_lib.py have
+the same size and field offsets as the structs gcc lays out from include/mli_hip.h, and the
+built libmli_hip.so loads and exports every entry point the header declares (no compute
+calls are made)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from mli_nerf_amd import _lib as L
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "mli_hip.h")
+
+STRUCTS = {
+    "mli_grid_levels": L.GridLevels, "mli_rays_args": L.RaysArgs, "mli_hashgrid_args": L.HashgridArgs,
+    "mli_sdf_args": L.SdfArgs, "mli_sample_coarse_args": L.SampleCoarseArgs,
+    "mli_sample_fine_args": L.SampleFineArgs, "mli_rgb_fwd_args": L.RgbFwdArgs,
+    "mli_composite_args": L.CompositeArgs, "mli_composite_bwd_args": L.CompositeBwdArgs,
+    "mli_rgb_bwd_args": L.RgbBwdArgs, "mli_wgrad_job": L.WgradJob, "mli_wgrad_args": L.WgradArgs,
+    "mli_pack_layer": L.PackLayer, "mli_pack_args": L.PackArgs, "mli_pack_sdf_args": L.PackSdfArgs,
+    "mli_assemble_layer": L.AssembleLayer, "mli_assemble_args": L.AssembleArgs,
+    "mli_adamw_args": L.AdamwArgs, "mli_cast_args": L.CastArgs,
+}
+
+
+def _declared_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(mli_\w+)\s*\(", src, re.M)))
+
+
+def test_struct_layout_matches_gcc(tmp_path):
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "mli_hip.h"', "int main(void) {"]
+    for cname, st in STRUCTS.items():
+        lines.append('printf("%s %%zu\\n", sizeof(%s));' % (cname, cname))
+        for f in st._fields_:
+            lines.append('printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (cname, f[0], cname, f[0]))
+    lines += ["return 0; }"]
+    c = tmp_path / "abi.c"
+    c.write_text("\n".join(lines))
+    exe = tmp_path / "abi"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.dirname(HEADER), str(c), "-o", str(exe)], check=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                  text=True).stdout.splitlines())
+    for cname, st in STRUCTS.items():
+        assert int(got[cname]) == C.sizeof(st), cname
+        for f in st._fields_:
+            assert int(got["%s.%s" % (cname, f[0])]) == getattr(st, f[0]).offset, (cname, f[0])
+
+
+def test_every_header_struct_is_mirrored():
+    src = open(HEADER).read()
+    declared = set(re.findall(r"}\s*(mli_\w+)\s*;", src))
+    assert declared == set(STRUCTS), declared ^ set(STRUCTS)
+
+
+def test_library_exports_header_entry_points():
+    if not os.path.exists(L.LIB_PATH):
+        pytest.skip("libmli_hip.so not built (run __graft_entry__.build())")
+    lib = L.lib()  # loads, binds argtypes and checks the ABI version
+    assert lib.mli_abi_version() == L.ABI_VERSION
+    fns = _declared_functions()
+    assert set(L.ENTRY_POINTS) | {"mli_abi_version", "mli_error_string"} == set(fns)
+    for name in fns:
+        assert hasattr(lib, name), name
+    assert lib.mli_error_string(0)
+
+
+def test_product_path_does_not_import_oracle():
+    pkg = os.path.join(ROOT, "mli_nerf_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for fn in files:
+            if fn.endswith(".py"):
+                txt = open(os.path.join(dirpath, fn)).read()
+                assert not re.search(r"^\s*(from|import)\s+oracle", txt, re.M), fn
