@@ -252,6 +252,7 @@ typedef struct {
   int n_layers;
   const mli_pack_layer* layers; /* DEVICE array of descriptors */
   uint8_t* dst;
+  float* row_scale;       /* scratch [n_layers][256]: g / ||v_row|| (n_out <= 256)           */
 } mli_pack_args;
 int mli_pack(const mli_pack_args* a, mli_stream_t s);
 

@@ -84,7 +84,7 @@ class PackLayer(C.Structure):
 
 
 class PackArgs(C.Structure):
-    _fields_ = [("n_layers", I32), ("layers", P), ("dst", P)]
+    _fields_ = [("n_layers", I32), ("layers", P), ("dst", P), ("row_scale", P)]
 
 
 class PackSdfArgs(C.Structure):

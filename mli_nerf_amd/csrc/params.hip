@@ -5,10 +5,26 @@
 namespace {
 
 // ---------------------------------------------------------------- pack
-// One thread per 16-byte fragment block (t, q, lane) of one layer (blockIdx.y), plus
-// 32 bias writers per n-tile (q == k_steps).  W = g * v / ||v||_row (torch weight_norm).
-__global__ __launch_bounds__(256) void pack_kernel(const mli_pack_layer* layers, uint8_t* dst) {
+// Row scales g[row] / ||v[row, :]|| of every layer (torch weight_norm dim=0), one wave per
+// row: blockIdx.y = layer, 4 rows per block.
+__global__ __launch_bounds__(256) void row_scale_kernel(const mli_pack_layer* layers, float* row_scale) {
   const mli_pack_layer& L = layers[blockIdx.y];
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= L.n_out) return;
+  const float* vr = L.v + (size_t)row * L.k_ref;
+  float ss = 0.f;
+  for (int k = lane; k < L.k_ref; k += 64) ss += vr[k] * vr[k];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+  if (lane == 0) row_scale[blockIdx.y * 256 + row] = L.g[row] / sqrtf(ss);
+}
+
+// One thread per 16-byte fragment block (t, q, lane) of one layer (blockIdx.y), plus
+// 32 bias writers per n-tile (q == k_steps).  W = v * row_scale.
+__global__ __launch_bounds__(256) void pack_kernel(const mli_pack_layer* layers, uint8_t* dst,
+                                                   const float* row_scale) {
+  const mli_pack_layer& L = layers[blockIdx.y];
+  const float* rs = row_scale + blockIdx.y * 256;
   const int per_tile = (L.k_steps + 1) * 64;
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= L.n_tiles * per_tile) return;
@@ -16,12 +32,6 @@ __global__ __launch_bounds__(256) void pack_kernel(const mli_pack_layer* layers,
   const int q = rem >> 6, lane = rem & 63;
   uint8_t* chunk = dst + L.dst_offset + (size_t)t * L.chunk_stride;
   const int rows_src = L.n_out, cols_src = L.k_ref;
-  auto wnorm_scale = [&](int row) {  // g[row] / ||v[row, :]||
-    const float* vr = L.v + (size_t)row * cols_src;
-    float ss = 0.f;
-    for (int k = 0; k < cols_src; ++k) ss += vr[k] * vr[k];
-    return L.g[row] / sqrtf(ss);
-  };
   if (q == L.k_steps) {  // bias block: [h][i] in accumulator order
     if (lane >= 32) return;
     const int hh = lane >> 4, i = lane & 15;
@@ -34,8 +44,7 @@ __global__ __launch_bounds__(256) void pack_kernel(const mli_pack_layer* layers,
   const int rl = lane & 31, hh = lane >> 5;
   const int n = 32 * t + rl;
   half8 out;
-  float sc_row = 0.f;
-  if (!L.transpose && n < rows_src) sc_row = wnorm_scale(n);
+  const float sc_row = (!L.transpose && n < rows_src) ? rs[n] : 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int kk = L.kmode[q] ? k_acc(q, hh, j) : k_nat(q, hh, j);
@@ -46,7 +55,7 @@ __global__ __launch_bounds__(256) void pack_kernel(const mli_pack_layer* layers,
         if (n < rows_src) w = L.v[(size_t)n * cols_src + src] * sc_row;
       } else {
         // A = W^T: row n indexes W's columns, packed k indexes W's rows (src)
-        if (n < cols_src) w = L.v[(size_t)src * cols_src + n] * wnorm_scale(src);
+        if (n < cols_src) w = L.v[(size_t)src * cols_src + n] * rs[src];
       }
     }
     out[j] = (f16)w;
@@ -122,8 +131,12 @@ __global__ __launch_bounds__(256) void cast_kernel(mli_cast_args a) {
 extern "C" int mli_pack(const mli_pack_args* a, mli_stream_t s) {
   // the host passes max threads over layers through n_layers' descriptors; size generously
   const int max_threads = 8 * (19 + 1) * 64;
+  if (a->n_layers <= 0) return 0;
+  if (a->row_scale == nullptr) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(row_scale_kernel, dim3(64, a->n_layers), dim3(256), 0, (hipStream_t)s, a->layers,
+                     a->row_scale);
   hipLaunchKernelGGL(pack_kernel, dim3((max_threads + 255) / 256, a->n_layers), dim3(256), 0,
-                     (hipStream_t)s, a->layers, a->dst);
+                     (hipStream_t)s, a->layers, a->dst, (const float*)a->row_scale);
   MLI_LAUNCH_CHECK();
 }
 

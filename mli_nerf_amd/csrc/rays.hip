@@ -264,46 +264,73 @@ __global__ __launch_bounds__(FW * 64) void sample_fine_kernel(FineArgs fa) {
 }
 
 // --------------------------------------------------------------------------- composite
-__global__ __launch_bounds__(128) void composite_fwd_kernel(mli_composite_args a) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= a.R) return;
+// One wave per ray, lane l owning samples 4l..4l+3 (N <= 256): NeuS alphas
+// (neuralangelo/model.py:492-515), exclusive transmittance by a wave product scan
+// (render.py:87-99), the composited sums by wave reductions (NeuralLumen/model.py:266-305).
+constexpr int CW = 4;  // rays per block
+__global__ __launch_bounds__(CW * 64) void composite_fwd_kernel(mli_composite_args a) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int R = a.R, N = a.N;
+  const int rr = blockIdx.x * CW + w;
+  if (rr >= R) return;  // whole wave exits (no block barriers below)
+  const int r = rr;
   const float inv_s = expf(a.s_var[0]);
   const float an = a.anneal;
   const float v0 = a.ray_unit[3 * r], v1 = a.ray_unit[3 * r + 1], v2 = a.ray_unit[3 * r + 2];
   const float far = a.far_[r];
-  float T = 1.f;
-  float rgb[3] = {0, 0, 0}, orr[3] = {0, 0, 0}, os = 0.f, op = 0.f, gr[3] = {0, 0, 0}, dep = 0.f;
-  float dk = a.dists[r];
-  for (int k = 0; k < N; ++k) {
-    const size_t s = (size_t)k * R + r;
-    const float dn = (k + 1 < N) ? a.dists[s + R] : far;
-    const float step = dn - dk;
-    const float g0 = a.grad[3 * s], g1 = a.grad[3 * s + 1], g2 = a.grad[3 * s + 2];
-    const float cosv = (v0 * g0 + v1 * g1) + v2 * g2;
-    // _get_iter_cos (neuralangelo/model.py:511-515)
-    const float ic = -(fmaxf(-cosv * 0.5f + 0.5f, 0.f) * (1.0f - an) + fmaxf(-cosv, 0.f) * an);
-    const float sd = a.sdf[s];
-    const float ep = sd - (ic * step) * 0.5f;
-    const float en = sd + (ic * step) * 0.5f;
-    const float cp = 1.0f / (1.0f + expf(-(ep * inv_s)));
-    const float cn = 1.0f / (1.0f + expf(-(en * inv_s)));
-    float al = (cp - cn) / (cp + 1e-5f);
-    al = fminf(fmaxf(al, 0.f), 1.f);
-    const float w = al * T;
-    T = T * (1.0f - al);
-    a.weights[s] = w;
-    const float* y = a.y + 8 * s;
-    for (int i = 0; i < 3; ++i) {
-      rgb[i] += y[i] * w;
-      orr[i] += y[3 + i] * w;
+  constexpr int E = 4;
+  float al[E], dk[E], g[E][3], wv[E];
+  float lp = 1.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int k = E * lane + e;
+    al[e] = 0.f; dk[e] = 0.f; g[e][0] = g[e][1] = g[e][2] = 0.f;
+    if (k < N) {
+      const size_t s = (size_t)k * R + r;
+      dk[e] = a.dists[s];
+      const float dn = (k + 1 < N) ? a.dists[s + R] : far;
+      const float step = dn - dk[e];
+      g[e][0] = a.grad[3 * s]; g[e][1] = a.grad[3 * s + 1]; g[e][2] = a.grad[3 * s + 2];
+      const float cosv = (v0 * g[e][0] + v1 * g[e][1]) + v2 * g[e][2];
+      // _get_iter_cos (neuralangelo/model.py:511-515)
+      const float ic = -(fmaxf(-cosv * 0.5f + 0.5f, 0.f) * (1.0f - an) + fmaxf(-cosv, 0.f) * an);
+      const float sd = a.sdf[s];
+      const float ep = sd - (ic * step) * 0.5f;
+      const float en = sd + (ic * step) * 0.5f;
+      const float cp = 1.0f / (1.0f + expf(-(ep * inv_s)));
+      const float cn = 1.0f / (1.0f + expf(-(en * inv_s)));
+      const float x = (cp - cn) / (cp + 1e-5f);
+      al[e] = fminf(fmaxf(x, 0.f), 1.f);
     }
-    os += y[6] * w;
-    op += w;
-    gr[0] += g0 * w; gr[1] += g1 * w; gr[2] += g2 * w;
-    dep += dk * w;
-    dk = dn;
+    lp *= 1.0f - al[e];
   }
+  float T = wave_excl_prod(lp, lane);
+  float acc[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) acc[i] = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int k = E * lane + e;
+    wv[e] = al[e] * T;
+    T = T * (1.0f - al[e]);
+    if (k < N) {
+      const size_t s = (size_t)k * R + r;
+      a.weights[s] = wv[e];
+      const f32x4 y0 = *reinterpret_cast<const f32x4*>(a.y + 8 * s);
+      const f32x4 y1 = *reinterpret_cast<const f32x4*>(a.y + 8 * s + 4);
+      acc[0] += y0[0] * wv[e]; acc[1] += y0[1] * wv[e]; acc[2] += y0[2] * wv[e];
+      acc[3] += y0[3] * wv[e]; acc[4] += y1[0] * wv[e]; acc[5] += y1[1] * wv[e];
+      acc[6] += y1[2] * wv[e];
+      acc[7] += wv[e];
+      acc[8] += g[e][0] * wv[e]; acc[9] += g[e][1] * wv[e]; acc[10] += g[e][2] * wv[e];
+      acc[11] += dk[e] * wv[e];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 12; ++i) acc[i] = wave_sum(acc[i]);
+  if (lane != 0) return;
+  float rgb[3] = {acc[0], acc[1], acc[2]}, orr[3] = {acc[3], acc[4], acc[5]}, os = acc[6];
+  const float op = acc[7];
   if (a.white_bg) {
     for (int i = 0; i < 3; ++i) {
       rgb[i] = rgb[i] + (1.f - op);
@@ -318,15 +345,19 @@ __global__ __launch_bounds__(128) void composite_fwd_kernel(mli_composite_args a
   }
   a.o_s[r] = os;
   if (a.opacity) a.opacity[r] = op;
-  if (a.gradient) for (int i = 0; i < 3; ++i) a.gradient[3 * r + i] = gr[i];
-  if (a.depth) a.depth[r] = dep / a.ray_norm[r];
+  if (a.gradient) for (int i = 0; i < 3; ++i) a.gradient[3 * r + i] = acc[8 + i];
+  if (a.depth) a.depth[r] = acc[11] / a.ray_norm[r];
 }
 
-__global__ __launch_bounds__(128) void composite_bwd_kernel(mli_composite_bwd_args a) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= a.R) return;
-  const int R = a.R, N = a.N;
-  float dr[3], dor[3], dos;
+// Backward of the composite + heads' output sigmoids: one thread per sample (no scan: the
+// gradient w.r.t. y only needs the forward weights), scaled by the power-of-two grad scale.
+__global__ __launch_bounds__(256) void composite_bwd_kernel(mli_composite_bwd_args a) {
+  const int R = a.R;
+  const size_t S = (size_t)R * a.N;
+  const size_t s = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (s >= S) return;
+  const int r = (int)(s % (size_t)R);
+  float dr[3], dor[3];
   const float os = a.o_s[r];
   float sre = 0.f;
   for (int i = 0; i < 3; ++i) {
@@ -335,20 +366,21 @@ __global__ __launch_bounds__(128) void composite_bwd_kernel(mli_composite_bwd_ar
     dor[i] = (a.d_o_r ? a.d_o_r[3 * r + i] : 0.f) - dre * os;
     sre += dre * a.o_r[3 * r + i];
   }
-  dos = (a.d_o_s ? a.d_o_s[r] : 0.f) - sre;
-  const float sc = a.grad_scale;
-  for (int k = 0; k < N; ++k) {
-    const size_t s = (size_t)k * R + r;
-    const float w = a.weights[s] * sc;
-    const float* y = a.y + 8 * s;
-    float* o = a.dz4 + 8 * s;
-    for (int i = 0; i < 3; ++i) {
-      o[i] = w * dr[i] * (y[i] * (1.f - y[i]));
-      o[3 + i] = w * dor[i] * (y[3 + i] * (1.f - y[3 + i]));
-    }
-    o[6] = w * dos * (y[6] * (1.f - y[6]));
-    o[7] = 0.f;
-  }
+  const float dos = (a.d_o_s ? a.d_o_s[r] : 0.f) - sre;
+  const float w = a.weights[s] * a.grad_scale;
+  const f32x4 y0 = *reinterpret_cast<const f32x4*>(a.y + 8 * s);
+  const f32x4 y1 = *reinterpret_cast<const f32x4*>(a.y + 8 * s + 4);
+  f32x4 o0, o1;
+  o0[0] = w * dr[0] * (y0[0] * (1.f - y0[0]));
+  o0[1] = w * dr[1] * (y0[1] * (1.f - y0[1]));
+  o0[2] = w * dr[2] * (y0[2] * (1.f - y0[2]));
+  o0[3] = w * dor[0] * (y0[3] * (1.f - y0[3]));
+  o1[0] = w * dor[1] * (y1[0] * (1.f - y1[0]));
+  o1[1] = w * dor[2] * (y1[1] * (1.f - y1[1]));
+  o1[2] = w * dos * (y1[2] * (1.f - y1[2]));
+  o1[3] = 0.f;
+  *reinterpret_cast<f32x4*>(a.dz4 + 8 * s) = o0;
+  *reinterpret_cast<f32x4*>(a.dz4 + 8 * s + 4) = o1;
 }
 
 }  // namespace
@@ -379,12 +411,14 @@ extern "C" int mli_sample_fine(const mli_sample_fine_args* a, mli_stream_t s) {
 
 extern "C" int mli_composite_fwd(const mli_composite_args* a, mli_stream_t s) {
   if (a->R <= 0) return 0;
-  hipLaunchKernelGGL(composite_fwd_kernel, dim3((a->R + 127) / 128), dim3(128), 0, (hipStream_t)s, *a);
+  if (a->N > 256) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(composite_fwd_kernel, dim3((a->R + CW - 1) / CW), dim3(CW * 64), 0, (hipStream_t)s, *a);
   MLI_LAUNCH_CHECK();
 }
 
 extern "C" int mli_composite_bwd(const mli_composite_bwd_args* a, mli_stream_t s) {
   if (a->R <= 0) return 0;
-  hipLaunchKernelGGL(composite_bwd_kernel, dim3((a->R + 127) / 128), dim3(128), 0, (hipStream_t)s, *a);
+  const size_t S = (size_t)a->R * a->N;
+  hipLaunchKernelGGL(composite_bwd_kernel, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, (hipStream_t)s, *a);
   MLI_LAUNCH_CHECK();
 }

@@ -112,8 +112,10 @@ class RenderEngine:
             bd = _to_device_structs(self._descs(self.bplan, tensors), self.device)
             self._pack_descs = (key, fd, bd, len(self.fplan), len(self.bplan))
         _, fd, bd, nf, nb = self._pack_descs
-        L.call("mli_pack", L.PackArgs(nf, L.ptr(fd), L.ptr(self.wfwd)))
-        L.call("mli_pack", L.PackArgs(nb, L.ptr(bd), L.ptr(self.wbwd)))
+        sf = self._buf("pack_scale_f", (nf, 256))
+        sb = self._buf("pack_scale_b", (nb, 256))
+        L.call("mli_pack", L.PackArgs(nf, L.ptr(fd), L.ptr(self.wfwd), L.ptr(sf)))
+        L.call("mli_pack", L.PackArgs(nb, L.ptr(bd), L.ptr(self.wbwd), L.ptr(sb)))
 
     def param_view(self, flat, name):
         off, shape = self.toff[name]

@@ -13,27 +13,37 @@ def _need_gpu():
         pytest.skip("no HIP device")
 
 
-@pytest.mark.parametrize("S", [8192, 65536])
+@pytest.mark.parametrize("S", [8192, 8384, 65536])
 def test_wgrad_matches_torch(S):
-    """dW = A B^T (fp32 accumulate), db = row sums of A, several jobs in one launch incl. thin."""
+    """dW = A B^T (fp32 accumulate), db = row sums of A: jobs of all three launch classes
+    (BIG 256x256, WIDE 256x320, THIN 32x256), a ragged sample count (8384 = 131 x 64) and a
+    job writing a column sub-range of a wider dW (ldw > K)."""
     _need_gpu()
     from mli_nerf_amd import _lib as L
     g = torch.Generator(device="cpu").manual_seed(3)
-    shapes = [(256, 304), (256, 256), (3, 256), (1, 256), (256, 256), (3, 256)]
+    shapes = [(256, 304), (256, 256), (3, 256), (1, 256), (256, 256), (3, 256), (256, 48)]
     jobs, refs = [], []
     keep = []
     for M, K in shapes:
         a = (torch.randn(M, S, generator=g) * 0.5).half().to(DEV)
         b = (torch.randn(K, S, generator=g) * 0.5).half().to(DEV)
-        dw = torch.zeros(M, K, device=DEV)
+        ldw = K + 40 if K == 48 else K
+        full = torch.zeros(M, ldw, device=DEV)
+        dw = full[:, 40:] if K == 48 else full
         db = torch.zeros(M, device=DEV)
-        keep += [a, b, dw, db]
-        jobs.append(L.WgradJob(L.ptr(a), L.ptr(b), M, K, L.ptr(dw), L.ptr(db)))
+        keep += [a, b, full, db]
+        jobs.append(L.WgradJob(L.ptr(a), L.ptr(b), M, K, L.ptr(dw), L.ptr(db), ldw))
         refs.append((a.float() @ b.float().t(), a.float().sum(1), dw, db))
+        if K == 48:
+            refs.append((torch.zeros(M, 40, device=DEV), torch.zeros(1, device=DEV), full[:, :40], None))
     arr = (L.WgradJob * len(jobs))(*jobs)
-    L.call("mli_wgrad", L.WgradArgs(S, len(jobs), C.cast(arr, C.c_void_p), 2048))
+    for cls in (1, 2, 4):
+        L.call("mli_wgrad", L.WgradArgs(S, len(jobs), C.cast(arr, C.c_void_p), cls))
     torch.cuda.synchronize()
     for i, (rw, rb, dw, db) in enumerate(refs):
+        if db is None:  # columns outside the job's range stay untouched
+            assert torch.equal(dw, rw)
+            continue
         err_w = ((dw - rw).abs().max() / rw.abs().max()).item()
         err_b = ((db - rb).abs().max() / rb.abs().max()).item()
         print("job %d %s: rel err dW %.2e db %.2e" % (i, tuple(rw.shape), err_w, err_b))
