@@ -4,7 +4,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmli_hip.so")
+# MLI_HIP_LIB selects an experiment build (tools/kbench.py A/B runs); default: the in-tree lib
+LIB_PATH = os.environ.get("MLI_HIP_LIB") or os.path.join(HERE, "libmli_hip.so")
 
 P = C.c_void_p
 I32 = C.c_int

@@ -14,8 +14,8 @@ FLAGS = ["-O3", "--offload-arch=gfx950", "-fPIC", "-std=c++17", "-ffp-contract=o
          "-I", os.path.join(REPO, "include"), "-I", CSRC]
 
 
-def _compile(src, extra):
-    obj = os.path.join(CSRC, "build", os.path.splitext(src)[0] + ".o")
+def _compile(src, extra, tag=""):
+    obj = os.path.join(CSRC, "build" + tag, os.path.splitext(src)[0] + ".o")
     os.makedirs(os.path.dirname(obj), exist_ok=True)
     cmd = [HIPCC] + FLAGS + list(extra) + ["-c", os.path.join(CSRC, src), "-o", obj]
     res = subprocess.run(cmd, capture_output=True, text=True)
@@ -24,24 +24,28 @@ def _compile(src, extra):
     return obj, res.stderr
 
 
-def build(verbose=False, extra=()):
+def build(verbose=False, extra=(), out=None):
+    """Compile + link; ``out``/``extra`` build an experiment variant (tools/, not the product)."""
+    out = out or OUT
+    tag = "" if out == OUT else "_" + os.path.splitext(os.path.basename(out))[0]
     deps = [os.path.join(CSRC, s) for s in SOURCES] + [
         os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + [
         os.path.join(REPO, "include", "mli_hip.h")]
-    if os.path.exists(OUT) and not extra and all(os.path.getmtime(d) <= os.path.getmtime(OUT) for d in deps):
-        return OUT
+    if os.path.exists(out) and not extra and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps):
+        return out
     with cf.ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
-        results = list(ex.map(lambda s: _compile(s, extra), SOURCES))
+        results = list(ex.map(lambda s: _compile(s, extra, tag), SOURCES))
     if verbose:
         for _, log in results:
             if log:
                 print(log)
     objs = [o for o, _ in results]
-    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT] + objs
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + objs
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError("link failed:\n" + res.stderr)
-    return OUT
+    return out
 
 
 if __name__ == "__main__":

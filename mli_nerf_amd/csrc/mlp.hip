@@ -11,66 +11,98 @@
 //    (ACC k-order, guide §3 "accumulator tile as the next MFMA's operand");
 //  * weights are pre-packed (mli_pack) into per-n-tile chunks of fp16 A fragments
 //    (1 KiB per k-step, one ds_read_b128 per MFMA) + 32 fp32 biases, laid out in exactly
-//    the order the kernel consumes them; all 8 waves share each chunk through a
-//    register-staged double-buffered LDS pipeline (global loads of chunk c+1 in flight
-//    while chunk c feeds the MFMAs).
+//    the order the kernel consumes them.  All 8 waves share each chunk through a 3-slot
+//    LDS ring filled by LDS-DMA (global_load_lds_dwordx4) two chunks ahead; each phase
+//    ends with a COUNTED vmcnt that retires only the next chunk's DMA (the activation
+//    stores issued since stay in flight: vmcnt counts loads and stores in issue order)
+//    and a raw s_barrier (no __syncthreads fence, which would drain the stores);
 //  * epilogues are fused: softplus(beta=100) for the SDF feature layer, ReLU (+ bit masks
 //    + feature-major activation stores for the weight gradients in training), sigmoid
-//    for the outputs.
+//    for the outputs.  Feature-major tiles are transposed through LDS so each 256-sample
+//    row leaves as 512 contiguous bytes.
 #include "common.h"
 
 namespace {
 
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_cvoid_t;
+
 constexpr int THREADS = 512;
 constexpr int WAVES = 8;
-constexpr int BUF = 20480;  // >= 19 KiB + 128 B (largest chunk), multiple of 256
 constexpr int CH(int ks) { return ks * 1024 + 128; }
 constexpr int FRAG_TILE = 16 * 64 * 8;  // halves per 32-sample tile of a 256-wide frag image
-// Feature-major activation tiles ([32 features][256 samples] fp16 per n-tile per workgroup)
-// are transposed through LDS so each row leaves as 512 contiguous bytes in 16 B stores.
-constexpr int SROW = 256 * 2 + 16;       // staged row stride (16 B pad)
+// weight ring: NSLOT slots of 3 x 8 KiB (one 16 B LDS-DMA per thread per 8 KiB round)
+constexpr int GLDS = 3;
+constexpr int SLOT = GLDS * 8192;       // >= CH(19) = 19584
+constexpr int NSLOT = 3;                // DMA distance 2 + the slot being read
+// feature-major staging ([32 features][256 samples] fp16 per n-tile), double buffered
+constexpr int SROW = 256 * 2 + 16;      // 16 B pad
 constexpr int STAGE = 32 * SROW;
-constexpr int LDS_BYTES = 2 * BUF + 2 * STAGE;
+constexpr int STAGE_OFF = NSLOT * SLOT;
+constexpr int MASK_OFF = STAGE_OFF + 2 * STAGE;  // backward: 2 x 8 KiB ReLU-mask blocks
+constexpr int LDS_FWD = STAGE_OFF + 2 * STAGE;
+constexpr int LDS_BWD = MASK_OFF + 2 * 8192;
 
-struct Pipe {
-  const uint8_t* next;
-  u32x4 st[3];
-  int bytes;
-  int buf;
+MLI_FI void glds16(const void* g, uint8_t* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_cvoid_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+// s_waitcnt vmcnt(n) for a count known after unrolling (the switch folds)
+MLI_FI void vm_wait(int n) {
+  switch (n) {
+#define MLI_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    MLI_VMW(1) MLI_VMW(2) MLI_VMW(3) MLI_VMW(4) MLI_VMW(5) MLI_VMW(6) MLI_VMW(7) MLI_VMW(8)
+    MLI_VMW(9) MLI_VMW(10) MLI_VMW(11) MLI_VMW(12)
+#undef MLI_VMW
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// LDS writes visible to the workgroup; no vector-memory drain (raw barrier).
+MLI_FI void block_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// ---------------------------------------------------------------------- weight ring
+struct Ring {
+  const uint8_t* src;   // source of chunk `next`
+  const uint8_t* last;  // source of the final chunk (dummy DMA past the end)
+  int next, n, cur;     // next chunk to issue, total chunks, chunk being consumed
 };
 
-MLI_FI void pipe_issue(Pipe& p, int bytes) {
-  p.bytes = bytes;
+// GLDS DMAs for chunk r.next into its slot (past the end: a dummy copy of the last chunk
+// into a free slot, so every phase issues the same count).  bytes(c) = size of chunk c.
+template <class Bytes>
+MLI_FI void ring_issue(Ring& r, uint8_t* lds, Bytes&& bytes) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool real = r.next < r.n;
+  const int nb = bytes(real ? r.next : r.n - 1);
+  const uint8_t* s = real ? r.src : r.last;
+  uint8_t* dst = lds + (r.next % NSLOT) * SLOT + wave * 1024;
 #pragma unroll
-  for (int u = 0; u < 3; ++u) {
-    const int o = min((u * THREADS + (int)threadIdx.x) * 16, bytes - 16);
-    p.st[u] = *reinterpret_cast<const u32x4*>(p.next + o);
-  }
+  for (int u = 0; u < GLDS; ++u) glds16(s + min(u * 8192 + wave * 1024 + lane * 16, nb - 16), dst + u * 8192);
+  if (real) r.src += nb;
+  r.next++;
 }
 
-MLI_FI void pipe_commit(Pipe& p, uint8_t* lds) {
-  uint8_t* dst = lds + (p.buf ^ 1) * BUF;
-#pragma unroll
-  for (int u = 0; u < 3; ++u) {
-    const int o = (u * THREADS + (int)threadIdx.x) * 16;
-    if (o < p.bytes) *reinterpret_cast<u32x4*>(dst + o) = p.st[u];
-  }
-  p.next += p.bytes;
-  p.bytes = 0;
+template <class Bytes>
+MLI_FI void ring_start(Ring& r, const void* base, int n, Bytes&& bytes) {
+  r.src = reinterpret_cast<const uint8_t*>(base);
+  size_t total = 0;
+  for (int c = 0; c + 1 < n; ++c) total += bytes(c);
+  r.last = r.src + total;
+  r.next = 0;
+  r.n = n;
+  r.cur = 0;
 }
 
-MLI_FI void pipe_start(Pipe& p, uint8_t* lds, int bytes) {
-  p.buf = 1;  // commit writes buffer 0
-  pipe_issue(p, bytes);
-  pipe_commit(p, lds);
-  p.buf = 0;
-  __syncthreads();
-}
-
-// Double-buffered LDS staging of feature-major tiles: stage_tile() writes a tile (the
-// accumulator layout: rows acc_row(i, h), sample column wave*32 + c) into one buffer; the
-// next workgroup barrier (inside run_layer) makes it visible and stage_flush() writes it
-// out while the other buffer takes the next tile.
+// ---------------------------------------------------------------------- LDS staging
+// stage_tile() writes a feature-major tile (accumulator layout: rows acc_row(i, h), sample
+// column wave*32 + c) into one buffer; the next phase's barrier makes it visible and
+// stage_flush() writes it out (16 B per lane, 512 B per row) while the other buffer takes
+// the next tile.
 struct Stager {
   uint16_t* pend;  // global address of (row 0, first sample of the block) of the staged tile
   int buf, pbuf;
@@ -78,7 +110,7 @@ struct Stager {
 
 MLI_FI void stage_tile(Stager& sg, uint8_t* lds, const f32x16& v, uint16_t* dst, int lane) {
   const int wave = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
-  uint8_t* sb = lds + 2 * BUF + sg.buf * STAGE + (4 * h) * SROW + (wave * 32 + c) * 2;
+  uint8_t* sb = lds + STAGE_OFF + sg.buf * STAGE + (4 * h) * SROW + (wave * 32 + c) * 2;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const f16 x = (f16)v[i];
@@ -90,9 +122,8 @@ MLI_FI void stage_tile(Stager& sg, uint8_t* lds, const f32x16& v, uint16_t* dst,
 }
 
 MLI_FI void stage_flush(Stager& sg, const uint8_t* lds, int S) {
-  if (sg.pend == nullptr) return;
   const int row = threadIdx.x >> 5, col = threadIdx.x & 31;
-  const uint8_t* sb = lds + 2 * BUF + sg.pbuf * STAGE;
+  const uint8_t* sb = lds + STAGE_OFF + sg.pbuf * STAGE;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int r = row + 16 * u;
@@ -116,37 +147,51 @@ MLI_FI f32x16 chunk_mma(const uint8_t* chunk, const half8* X, int lane) {
   const half8* w = reinterpret_cast<const half8*>(chunk) + lane;
 #pragma unroll
   for (int q = 0; q < KS; ++q) acc = mfma32(w[q * 64], X[q], acc);
-  // keep at most RA weight fragments in flight (register pressure): RA reads, then one
-  // read per MFMA
-  constexpr int RA = KS < 4 ? KS : 4;
-  __builtin_amdgcn_sched_group_barrier(0x100, RA, 0);
-#pragma unroll
-  for (int q = 0; q < KS; ++q) {
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    if (q + RA < KS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-  }
   return acc;
 }
 
-// One layer of NT n-tiles over KS k-steps; `next_bytes` = size of the chunk after this layer.
-// epi(t, acc) consumes each finished tile.
-template <int KS, int NT, class Epi>
-MLI_FI void run_layer(Pipe& p, uint8_t* lds, Stager& sg, int S, const half8* X, int lane, int next_bytes,
-                      Epi&& epi) {
+// One layer of NT n-tiles over KS k-steps; epi(t, acc) consumes each finished tile.
+// Static store counts (for the counted vmcnt): STAGED = the layer stages its tiles (the
+// flush of tile t-1 at t >= 1 is 2 stores; the flush at t == 0 is decided at run time and
+// not counted), EPI = unconditional global stores per epilogue, MASKED = one mask store at
+// t == NT-1; pre(t) issues (and returns the count of) VMEM ops ahead of the weight DMAs.
+template <int KS, int NT, bool STAGED, int EPI, bool MASKED, class Bytes, class Pre, class Epi>
+MLI_FI void run_layer(Ring& rg, uint8_t* lds, Stager& sg, int S, const half8* X, int lane, Bytes&& bytes,
+                      Pre&& pre, Epi&& epi) {
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const int nb = (t + 1 < NT) ? CH(KS) : next_bytes;
-    if (nb) pipe_issue(p, nb);
-    const f32x16 acc = chunk_mma<KS>(lds + p.buf * BUF, X, lane);
-    if (nb) pipe_commit(p, lds);
-    __syncthreads();
-    p.buf ^= 1;
-    stage_flush(sg, lds, S);
+    const int npre = pre(t);
+    ring_issue(rg, lds, bytes);
+    if (t == 0) {
+      if (sg.pend) stage_flush(sg, lds, S);
+    } else if (STAGED) {
+      stage_flush(sg, lds, S);
+    }
+    const f32x16 acc = chunk_mma<KS>(lds + (rg.cur % NSLOT) * SLOT, X, lane);
     epi(t, acc);
+    // ops younger than chunk cur+1's DMAs (issued one phase earlier): this phase's mask DMAs,
+    // weight DMAs, flush and epilogue stores, plus the previous phase's flush and epilogue
+    const int f_now = (t > 0 && STAGED) ? 2 : 0;
+    const int f_prev = (t > 1 && STAGED) ? 2 : 0;
+    const int e_now = EPI + ((MASKED && t == NT - 1) ? 1 : 0);
+    const int e_prev = t > 0 ? EPI : 0;
+    vm_wait(npre + GLDS + f_now + e_now + f_prev + e_prev);
+    block_sync();
+    rg.cur++;
   }
 }
 
+struct NoPre {
+  MLI_FI int operator()(int) const { return 0; }
+};
+
 // ---------------------------------------------------------------------- forward
+// chunk sizes in consumption order: SDF layer 1 (8 x KS 16), then per head L0 (8 x KS 19),
+// L1..L3 (24 x KS 16), L4 (1 x KS 16)
+MLI_FI int fwd_bytes(int c) { return (c >= 8 && (c - 8) % 33 < 8) ? CH(19) : CH(16); }
+constexpr int FWD_CHUNKS = 8 + 3 * 33;
+
+template <bool TRAIN>
 __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -156,7 +201,10 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
   const int m = tile * 32 + c;
   const int r = m / a.N, k = m - r * a.N;
   const size_t slot = (size_t)k * a.R + r;
-  const bool train = a.xT != nullptr;
+  auto bytes = [](int cc) MLI_LAMBDA_FI { return fwd_bytes(cc); };
+
+  Ring rg;
+  ring_start(rg, a.wfwd, FWD_CHUNKS, bytes);
 
   half8 A[16], B[19];
   // h0 frags (SDF layer-0 activations) -> B[0..15]
@@ -192,7 +240,7 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
       B[16][j] = (f16)v16;
       B[17][j] = (f16)v17;
       B[18][j] = (f16)v18;
-      if (train) {
+      if (TRAIN) {
         // feature-major rows 256..303 (k_nat order) from the fp32 sources
         a.x0T[(size_t)k_nat(16, h, j) * S + m] = __builtin_bit_cast(uint16_t, (f16)v16);
         a.x0T[(size_t)k_nat(17, h, j) * S + m] = __builtin_bit_cast(uint16_t, (f16)v17);
@@ -200,16 +248,19 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
       }
     }
   }
+  // prologue: chunks 0 and 1 in flight, wait for chunk 0
+  ring_issue(rg, lds, bytes);
+  ring_issue(rg, lds, bytes);
+  vm_wait(GLDS);
+  block_sync();
 
-  Pipe pipe;
-  pipe.next = reinterpret_cast<const uint8_t*>(a.wfwd);
-  pipe_start(pipe, lds, CH(16));
   Stager sg{nullptr, 0, 0};
   const size_t col0 = (size_t)blockIdx.x * 256;
 
   // SDF layer 1: feat = softplus(W1 h0 + b1) -> A; frag image scratch (+ x0T rows 0..255)
   uint16_t* ftile = a.feat_frag + (size_t)tile * FRAG_TILE;
-  run_layer<16, 8>(pipe, lds, sg, S, B, lane, CH(19), [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
+  run_layer<16, 8, TRAIN, 2, false>(rg, lds, sg, S, B, lane, bytes, NoPre{},
+                                    [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
     f32x16 v;
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = softplus100(acc[i]);
@@ -218,7 +269,7 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
     half8* dst = reinterpret_cast<half8*>(ftile) + (2 * t) * 64 + lane;
     dst[0] = A[2 * t];
     dst[64] = A[2 * t + 1];
-    if (train) stage_tile(sg, lds, v, a.x0T + (size_t)(32 * t) * S + col0, lane);
+    if (TRAIN) stage_tile(sg, lds, v, a.x0T + (size_t)(32 * t) * S + col0, lane);
   });
 
   for (int hd = 0; hd < 3; ++hd) {
@@ -238,7 +289,7 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
         for (int i = 0; i < 16; ++i) v[i] = fmaxf(acc[i], 0.0f);
         out[2 * t] = acc_to_frag(v, 0);
         out[2 * t + 1] = acc_to_frag(v, 1);
-        if (train) {
+        if (TRAIN) {
           uint32_t bits = 0;
 #pragma unroll
           for (int i = 0; i < 16; ++i) bits |= (acc[i] > 0.0f ? 1u : 0u) << i;
@@ -252,14 +303,14 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
         }
       };
     };
-    run_layer<19, 8>(pipe, lds, sg, S, B, lane, CH(16), relu_epi(A, 0));
-    run_layer<16, 8>(pipe, lds, sg, S, A, lane, CH(16), relu_epi(B, 1));
-    run_layer<16, 8>(pipe, lds, sg, S, B, lane, CH(16), relu_epi(A, 2));
-    run_layer<16, 8>(pipe, lds, sg, S, A, lane, CH(16), relu_epi(B, 3));
-    const int after = (hd < 2) ? CH(19) : 0;
+    run_layer<19, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, B, lane, bytes, NoPre{}, relu_epi(A, 0));
+    run_layer<16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, A, lane, bytes, NoPre{}, relu_epi(B, 1));
+    run_layer<16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, B, lane, bytes, NoPre{}, relu_epi(A, 2));
+    run_layer<16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, A, lane, bytes, NoPre{}, relu_epi(B, 3));
     const int no = hd == 2 ? 1 : 3;
     const int off = hd * 3;
-    run_layer<16, 1>(pipe, lds, sg, S, B, lane, after, [&](int, const f32x16& acc) MLI_LAMBDA_FI {
+    run_layer<16, 1, false, 0, false>(rg, lds, sg, S, B, lane, bytes, NoPre{},
+                                      [&](int, const f32x16& acc) MLI_LAMBDA_FI {
       if (h == 0) {
 #pragma unroll
         for (int i = 0; i < 3; ++i)
@@ -267,9 +318,14 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
       }
     });
   }
+  vm_wait(0);  // no LDS-DMA may land after the workgroup's LDS is released
 }
 
 // ---------------------------------------------------------------------- backward dX chain
+// chunk sizes: per head W4^T (8 x KS 1), W3^T, W2^T, W1^T (24 x KS 16)
+MLI_FI int bwd_bytes(int c) { return (c % 32) < 8 ? CH(1) : CH(16); }
+constexpr int BWD_CHUNKS = 3 * 32;
+
 __global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -280,11 +336,26 @@ __global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
   const int m = tile * 32 + c;
   const int r = m / a.N, k = m - r * a.N;
   const size_t slot = (size_t)k * a.R + r;
+  auto bytes = [](int cc) MLI_LAMBDA_FI { return bwd_bytes(cc); };
+  // ReLU-mask block of global layer L (= head*4 + li, li = 0..3 runs masks 3, 2, 1, 0): the
+  // workgroup's 8 tiles are contiguous (8 KiB); one 16 B DMA per thread into mask slot L&1
+  auto mask_dma = [&](int L) MLI_LAMBDA_FI {
+    const int Lc = min(L, 11);
+    const int hd = Lc >> 2, ml = 3 - (Lc & 3);
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(a.masks) +
+                         (((size_t)(hd * 4 + ml) * tiles + (size_t)blockIdx.x * WAVES) * 64) * 16;
+    glds16(src + threadIdx.x * 16, lds + MASK_OFF + (L & 1) * 8192 + wave * 1024);
+  };
+
+  Ring rg;
+  ring_start(rg, a.wbwd, BWD_CHUNKS, bytes);
+  mask_dma(0);
+  ring_issue(rg, lds, bytes);
+  ring_issue(rg, lds, bytes);
+  vm_wait(GLDS);
+  block_sync();
 
   half8 A[16], B[16];
-  Pipe pipe;
-  pipe.next = reinterpret_cast<const uint8_t*>(a.wbwd);
-  pipe_start(pipe, lds, CH(1));
   Stager sg{nullptr, 0, 0};
   const size_t col0 = (size_t)blockIdx.x * 256;
   for (int hd = 0; hd < 3; ++hd) {
@@ -305,12 +376,21 @@ __global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
           }
       }
     }
-    auto mask_epi = [&](half8* out, int layer /* dZ index */, int mask_layer) MLI_LAMBDA_FI {
-      return [&, out, layer, mask_layer](int t, const f32x16& acc) MLI_LAMBDA_FI {
-        const u32x4 mv = *(reinterpret_cast<const u32x4*>(a.masks) +
-                           ((size_t)(hd * 4 + mask_layer) * tiles + tile) * 64 + lane);
-        const uint32_t words[4] = {mv[0], mv[1], mv[2], mv[3]};
-        const uint32_t bits = words[t >> 1] >> ((t & 1) * 16);
+    // the phase at t == 6 issues the next layer's mask DMA (before its weight DMAs)
+    auto pre = [&](int li) MLI_LAMBDA_FI {
+      return [&, li](int t) MLI_LAMBDA_FI {
+        if (t != 6) return 0;
+        mask_dma(hd * 4 + li + 1);
+        return 1;
+      };
+    };
+    auto mask_epi = [&](half8* out, int layer /* dZ index */, int li) MLI_LAMBDA_FI {
+      return [&, out, layer, li](int t, const f32x16& acc) MLI_LAMBDA_FI {
+        const u32x4 mv =
+            *reinterpret_cast<const u32x4*>(lds + MASK_OFF + (li & 1) * 8192 + wave * 1024 + lane * 16);
+        const int wi = t >> 1;
+        const uint32_t word = wi == 0 ? mv[0] : wi == 1 ? mv[1] : wi == 2 ? mv[2] : mv[3];
+        const uint32_t bits = word >> ((t & 1) * 16);
         f32x16 v;
 #pragma unroll
         for (int i = 0; i < 16; ++i) v[i] = ((bits >> i) & 1u) ? acc[i] : 0.0f;
@@ -319,13 +399,13 @@ __global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
         stage_tile(sg, lds, v, a.dzT + ((size_t)(hd * 4 + layer) * 256 + 32 * t) * S + col0, lane);
       };
     };
-    run_layer<1, 8>(pipe, lds, sg, S, &z4, lane, CH(16), mask_epi(A, 3, 3));
-    run_layer<16, 8>(pipe, lds, sg, S, A, lane, CH(16), mask_epi(B, 2, 2));
-    run_layer<16, 8>(pipe, lds, sg, S, B, lane, CH(16), mask_epi(A, 1, 1));
-    run_layer<16, 8>(pipe, lds, sg, S, A, lane, hd < 2 ? CH(1) : 0, mask_epi(B, 0, 0));
+    run_layer<1, 8, true, 0, false>(rg, lds, sg, S, &z4, lane, bytes, pre(0), mask_epi(A, 3, 0));
+    run_layer<16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, pre(1), mask_epi(B, 2, 1));
+    run_layer<16, 8, true, 0, false>(rg, lds, sg, S, B, lane, bytes, pre(2), mask_epi(A, 1, 2));
+    run_layer<16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, pre(3), mask_epi(B, 0, 3));
   }
-  __syncthreads();
-  stage_flush(sg, lds, opaque_s(a.R * a.N));
+  stage_flush(sg, lds, opaque_s(a.R * a.N));  // the last tile, made visible by the last phase's barrier
+  vm_wait(0);
 }
 
 }  // namespace
@@ -333,13 +413,18 @@ __global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
 extern "C" int mli_rgb_fwd(const mli_rgb_fwd_args* a, mli_stream_t s) {
   const int S = a->R * a->N;
   if (S % 256 != 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(rgb_fwd_kernel, dim3(S / 256), dim3(THREADS), LDS_BYTES, (hipStream_t)s, *a);
+  const bool train = a->xT != nullptr;
+  if (train && (a->x0T == nullptr || a->masks == nullptr)) return (int)hipErrorInvalidValue;
+  if (train)
+    hipLaunchKernelGGL(rgb_fwd_kernel<true>, dim3(S / 256), dim3(THREADS), LDS_FWD, (hipStream_t)s, *a);
+  else
+    hipLaunchKernelGGL(rgb_fwd_kernel<false>, dim3(S / 256), dim3(THREADS), LDS_FWD, (hipStream_t)s, *a);
   MLI_LAUNCH_CHECK();
 }
 
 extern "C" int mli_rgb_bwd(const mli_rgb_bwd_args* a, mli_stream_t s) {
   const int S = a->R * a->N;
   if (S % 256 != 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(rgb_bwd_kernel, dim3(S / 256), dim3(THREADS), LDS_BYTES, (hipStream_t)s, *a);
+  hipLaunchKernelGGL(rgb_bwd_kernel, dim3(S / 256), dim3(THREADS), LDS_BWD, (hipStream_t)s, *a);
   MLI_LAUNCH_CHECK();
 }
