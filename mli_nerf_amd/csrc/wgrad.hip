@@ -49,7 +49,7 @@ MLI_FI void stage_store(const u32x4 (&st)[LOADS], uint8_t* lds, int tid) {
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int DEPTH>
 __global__ __launch_bounds__(512) void wgrad_kernel(KArgs ka) {
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -73,9 +73,9 @@ __global__ __launch_bounds__(512) void wgrad_kernel(KArgs ka) {
   const int h = lane >> 5, rl = lane & 31;
   const size_t S = ka.S;
 
-  // staging map: 8 x 16 B per row of BK samples
+  // staging map: 8 x 16 B per row of BK samples; DEPTH register sets in flight
   constexpr int A_LOADS = (BM * 8 + 511) / 512, B_LOADS = (BN * 8 + 511) / 512;
-  u32x4 sa[A_LOADS], sb[B_LOADS];
+  u32x4 sa[DEPTH][A_LOADS], sb[DEPTH][B_LOADS];
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -86,18 +86,18 @@ __global__ __launch_bounds__(512) void wgrad_kernel(KArgs ka) {
   const bool do_bias = (J.db != nullptr) && tn == 0;
   float bsum = 0.f;  // row (tid >> 1) of the A tile, half (tid & 1)
 
-  stage_load<BM, A_LOADS>(sa, J.a, J.M, tm, S, k0, tid);
-  stage_load<BN, B_LOADS>(sb, J.b, J.K, tn, S, k0, tid);
-  for (int kk = k0; kk < k1; kk += BK) {
+  // clamped prefetch: past the slice end it reloads the last valid k-step (never consumed)
+  auto load = [&](int d, int kk) MLI_LAMBDA_FI {
+    const int kc = min(kk, k1 - BK);
+    stage_load<BM, A_LOADS>(sa[d], J.a, J.M, tm, S, kc, tid);
+    stage_load<BN, B_LOADS>(sb[d], J.b, J.K, tn, S, kc, tid);
+  };
+  auto step = [&](int d, int kk) MLI_LAMBDA_FI {
     __syncthreads();
-    stage_store<BM, A_LOADS>(sa, la, tid);
-    stage_store<BN, B_LOADS>(sb, lb, tid);
+    stage_store<BM, A_LOADS>(sa[d], la, tid);
+    stage_store<BN, B_LOADS>(sb[d], lb, tid);
     __syncthreads();
-    {  // prefetch the next k-step (clamped: the last iteration reloads a valid slice)
-      const int kn = min(kk + BK, k1 - BK);
-      stage_load<BM, A_LOADS>(sa, J.a, J.M, tm, S, kn, tid);
-      stage_load<BN, B_LOADS>(sb, J.b, J.K, tn, S, kn, tid);
-    }
+    load(d, kk + DEPTH * BK);
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
       half8 fa[TM], fb[TN];
@@ -121,6 +121,14 @@ __global__ __launch_bounds__(512) void wgrad_kernel(KArgs ka) {
         for (int e = 0; e < 8; ++e) bsum += (float)v[e];
       }
     }
+  };
+
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d) load(d, k0 + d * BK);
+  for (int kk = k0; kk < k1; kk += DEPTH * BK) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d)
+      if (kk + d * BK < k1) step(d, kk + d * BK);
   }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -147,7 +155,7 @@ inline int job_class(const mli_wgrad_job& j) {
 
 // One launch per class: tiles of all its jobs x n_split k-slices, n_split sized so the
 // grid holds about OCC workgroups per CU (OCC = resident 512-thread workgroups per CU).
-template <int BM, int BN, int WM, int WN, int OCC>
+template <int BM, int BN, int WM, int WN, int OCC, int DEPTH>
 int launch(const mli_wgrad_args* a, int cls, hipStream_t s) {
   KArgs ka;
   ka.S = a->S;
@@ -172,7 +180,7 @@ int launch(const mli_wgrad_args* a, int cls, hipStream_t s) {
     ka.jobs[i].tile_base = base;
     base += ((ka.jobs[i].M + BM - 1) / BM) * ka.jobs[i].tiles_n * ka.n_split;
   }
-  hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN>), dim3(base), dim3(512), (BM + BN) * ROWB, s, ka);
+  hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, DEPTH>), dim3(base), dim3(512), (BM + BN) * ROWB, s, ka);
   return (int)hipGetLastError();
 }
 
@@ -181,8 +189,8 @@ int launch(const mli_wgrad_args* a, int cls, hipStream_t s) {
 extern "C" int mli_wgrad(const mli_wgrad_args* a, mli_stream_t s) {
   if (a->S <= 0 || a->S % BK != 0) return (int)hipErrorInvalidValue;
   int e = 0;
-  if (a->classes & CLS_BIG) e = launch<256, 256, 4, 2, 1>(a, CLS_BIG, (hipStream_t)s);
-  if (!e && (a->classes & CLS_WIDE)) e = launch<256, 320, 4, 2, 1>(a, CLS_WIDE, (hipStream_t)s);
-  if (!e && (a->classes & CLS_THIN)) e = launch<32, 256, 1, 8, 2>(a, CLS_THIN, (hipStream_t)s);
+  if (a->classes & CLS_BIG) e = launch<256, 256, 4, 2, 1, 2>(a, CLS_BIG, (hipStream_t)s);
+  if (!e && (a->classes & CLS_WIDE)) e = launch<256, 320, 4, 2, 1, 1>(a, CLS_WIDE, (hipStream_t)s);
+  if (!e && (a->classes & CLS_THIN)) e = launch<32, 256, 1, 8, 2, 2>(a, CLS_THIN, (hipStream_t)s);
   return e;
 }

@@ -108,6 +108,18 @@ class FusedAdamW:
         self.v.copy_(sd["exp_avg_sq"])
 
 
+def reduce_gradients(grad, world_size, group=None):
+    """Data-parallel gradient average = DDP's bucketed all-reduce (imaginaire wraps the model
+    in DistributedDataParallel, imaginaire/trainers/utils/get_trainer.py:81): the whole trainable state
+    is ONE flat fp32 buffer (3.2 MB), so it goes as ONE all-reduce (RCCL over xGMI on the
+    MI355X node, gloo in the CPU tests), then / world_size."""
+    if world_size > 1:
+        import torch.distributed as dist
+        dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=group)
+        grad.div_(world_size)
+    return grad
+
+
 class Trainer:
     """Minimal stage-b trainer: ``train_step(data)`` = forward + loss + backward + AdamW."""
 
@@ -145,11 +157,7 @@ class Trainer:
         out = self.model(data, u=u)
         total, losses, psnr = stage_b_losses(out, data, self.weights, self.ranges, self.re_factors)
         total.backward()
-        grad = self.model.flat.grad
-        if self.world_size > 1:
-            import torch.distributed as dist
-            dist.all_reduce(grad, op=dist.ReduceOp.SUM)
-            grad.div_(self.world_size)
+        grad = reduce_gradients(self.model.flat.grad, self.world_size)
         self.optim.step(grad, self.lr())
         self.current_iteration += 1
         self.losses = {k: v.detach() for k, v in losses.items()}
