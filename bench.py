@@ -44,9 +44,131 @@ def kernel_flops(name, R, N, Nc, Nf, H):
         return 2 * S * sum(HIDDEN * o + 3 * HIDDEN * HIDDEN for o in HEAD_OUT)
     if name == "mli_wgrad":
         return 2 * S * heads_fwd
+    if name == "mli_wgrad:big":    # dW of the 256x256 hidden layers L1..L3 of the 3 heads
+        return 2 * S * 3 * 3 * HIDDEN * HIDDEN
+    if name == "mli_wgrad:wide":   # dW of layer 0 (294 / 262 / 278 inputs)
+        return 2 * S * HIDDEN * sum(HEAD_IN)
+    if name == "mli_wgrad:thin":   # dW of the output layers (3 / 3 / 1 rows)
+        return 2 * S * HIDDEN * sum(HEAD_OUT)
     if name == "mli_sdf:field":
         return 5 * S * sdf_point
     return 0
+
+
+def kernel_table(prof, n_units, R, N, fine):
+    """Per-call-name HIP-event timings -> table + roofline record of the dominant MFMA call."""
+    kernels = {}
+    for name, e0, e1 in prof or []:
+        k = kernels.setdefault(name, [0.0, 0])
+        k[0] += e0.elapsed_time(e1)
+        k[1] += 1
+    ktab = {n: {"ms_per_launch": v[0] / v[1], "launches_per_unit": v[1] / n_units,
+                "ms_per_unit": v[0] / n_units} for n, v in sorted(kernels.items(), key=lambda kv: -kv[1][0])}
+    roof = None
+    mfma = [n for n in ktab if kernel_flops(n, R, N, 64, fine, 4) > 0]
+    if mfma:
+        dom = max(mfma, key=lambda n: ktab[n]["ms_per_unit"])
+        fl = kernel_flops(dom, R, N, 64, fine, 4)
+        achieved = fl / (ktab[dom]["ms_per_launch"] * 1e-3) / 1e12
+        roof = {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F16_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_F16_TFLOPS, 4), "traffic": None,
+                "flops_per_launch": fl}
+        for n in ktab:
+            f = kernel_flops(n, R, N, 64, fine, 4)
+            if f:
+                ktab[n]["tflops"] = round(f / (ktab[n]["ms_per_launch"] * 1e-3) / 1e12, 2)
+    return ktab, roof
+
+
+def run_infer(args, world, rank, dev):
+    """configs[4]: syn_hotdog_b video_train inference, size x size frames rendered in
+    `chunk`-ray chunks, tile-sharded over the ranks with one all_gather per frame
+    (Model.inference); rays/s = frames * size^2 / wall time (strong scaling)."""
+    from mli_nerf_amd import _lib as L, synthetic
+    from mli_nerf_amd.configs import preset
+    from mli_nerf_amd.model import Model
+    size = args.size
+    cfg = preset(args.config, n_fine=args.fine,
+                 overrides={"data": {"train": {"image_size": [size, size]}, "val": {"image_size": [size, size]}},
+                            "model": {"render": {"rand_rays_val": args.chunk}}})
+    model = Model(cfg.model, cfg.data)
+    model.load_state_dict(synthetic.make_state_dict(log2T=22, seed=0))
+    model = model.to(dev)
+    N = model.pcfg.n_samples
+    frames = [{k: v.to(dev) for k, v in synthetic.make_batch(1, H=size, W=size, frame=f).items()}
+              for f in range(args.warmup + args.frames)]
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    for f in range(args.warmup):
+        model.inference(frames[f])
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    if not args.no_kernel_timing:
+        L.PROFILE = []
+    t0 = time.perf_counter()
+    out = None
+    for f in range(args.warmup, args.warmup + args.frames):
+        out = model.inference(frames[f])
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    prof, L.PROFILE = L.PROFILE, None
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    n_pix = size * size
+    value = n_pix * args.frames / elapsed
+    R_chunk = min(args.chunk, -(-n_pix // world))
+    ktab, roof = kernel_table(prof, args.frames, R_chunk, N, args.fine)
+    result = {
+        "metric": "rays/sec, syn_hotdog_b video_train inference %dx%d full frame (configs[4])" % (size, size),
+        "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": args.frames,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.frames * 1e3, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f16 MFMA (fp32 accumulate) / fp32",
+        "data": "synthetic (seeded cameras/lights, random-init weights, full 2^22 hash table)",
+        "config": {"workload": "%s inference, %dx%d frames, %d-ray chunks, tile-sharded" % (args.config, size, size,
+                                                                                            args.chunk),
+                   "samples_per_ray": N, "frames": args.frames, "parallelism": "tiles%d" % world},
+        "roofline": roof, "kernels": ktab,
+        "rgb_mean": round(float(out["rgb"].mean()), 5),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        # CPU oracle eval forward on a bounded sample of the same frame's rays
+        from oracle import render as o_render
+        threads = min(16, os.cpu_count() or 1)
+        torch.set_num_threads(threads)
+        sd = synthetic.make_state_dict(log2T=22, seed=0)
+        pcfg = o_render.PathCfg(n_fine=args.fine)
+        data = {k: v.cpu() for k, v in frames[args.warmup].items()}
+        n_cpu = args.cpu_rays * 4
+        data["ray_idx"] = torch.arange(n_cpu)[None] * (n_pix // n_cpu)
+        with torch.no_grad():
+            o_render.forward(sd, pcfg, data, u=None, training=False, width=size, height=size)
+            t1 = time.perf_counter()
+            ref = o_render.forward(sd, pcfg, data, u=None, training=False, width=size, height=size)
+            t_cpu = time.perf_counter() - t1
+        result["cpu_baseline"] = {"value": round(n_cpu / t_cpu, 3), "unit": "rays/s", "cores": threads,
+                                  "kind": "port", "sample": "oracle eval forward, %d rays of one %dx%d frame x %d "
+                                  "samples, full hash table, torch fp32 on %d host threads" % (n_cpu, size, size, N,
+                                                                                             threads)}
+        result["speedup_vs_cpu"] = round(value / result["cpu_baseline"]["value"], 1)
+        gpu_rgb = out["rgb"][0].cpu()[data["ray_idx"][0]]
+        d = (gpu_rgb - ref["rgb"][0]).abs()
+        result["rgb_check"] = {"rays": n_cpu, "max_abs": round(float(d.max()), 6),
+                               "psnr_of_diff_db": round(-10 * math.log10(max(float((d ** 2).mean()), 1e-20)), 2)}
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
 
 def cpu_baseline(R_cpu, steps, threads):
@@ -62,19 +184,19 @@ def cpu_baseline(R_cpu, steps, threads):
     u = synthetic.stratified_uniforms(R_cpu, pcfg.n_coarse, seed=7)
     times = []
     out = psnr = None
-    for i in range(steps + 1):
+    for i in range(steps + 2):  # 2 untimed warm-up steps
         t0 = time.perf_counter()
         out = o_render.forward(sd, pcfg, data, u=u, training=True, progress=0.0)
         total, _, psnr = o_render.stage_b_losses(out, data, pcfg)
         total.backward()
         for v in sd.values():
             v.grad = None
-        if i > 0:
+        if i > 1:
             times.append(time.perf_counter() - t0)
     t = sum(times) / len(times)
     return dict(value=R_cpu / t, unit="rays/s", cores=threads, kind="port",
                 sample="oracle fwd+bwd stage-b, %d rays x %d samples, full hash table, %d timed steps "
-                       "after 1 warm-up, torch fp32 on %d host threads" % (R_cpu, pcfg.n_samples, steps, threads),
+                       "after 2 warm-up, torch fp32 on %d host threads" % (R_cpu, pcfg.n_samples, steps, threads),
                 s_per_step=t), data, u, float(psnr)
 
 
@@ -86,10 +208,15 @@ def main():
     ap.add_argument("--config", default="syn_hotdog_b")
     ap.add_argument("--rays", type=int, default=4096)
     ap.add_argument("--fine", type=int, default=16)
-    ap.add_argument("--cpu-rays", type=int, default=256)
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-rays", type=int, default=512)
+    ap.add_argument("--cpu-steps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--mode", choices=("train", "infer"), default="train",
+                    help="train: BASELINE configs[1] step; infer: configs[4] full-frame render")
+    ap.add_argument("--frames", type=int, default=4, help="infer: frames timed (after --warmup frames)")
+    ap.add_argument("--size", type=int, default=800, help="infer: frame is size x size")
+    ap.add_argument("--chunk", type=int, default=20000, help="infer: rand_rays_val")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -106,6 +233,8 @@ def main():
     from mli_nerf_amd.configs import preset
     from mli_nerf_amd.model import Model
     from mli_nerf_amd.trainer import Trainer
+    if args.mode == "infer":
+        return run_infer(args, world, rank, dev)
 
     cfg = preset(args.config, rays=args.rays, n_fine=args.fine)
     model = Model(cfg.model, cfg.data)
@@ -144,27 +273,7 @@ def main():
     psnr = trainer.metrics["psnr"].item()
     loss = trainer.losses["total"].item()
 
-    kernels = {}
-    if prof:
-        for name, e0, e1 in prof:
-            k = kernels.setdefault(name, [0.0, 0])
-            k[0] += e0.elapsed_time(e1)
-            k[1] += 1
-    ktab = {n: {"ms_per_launch": v[0] / v[1], "launches_per_step": v[1] / args.steps,
-                "ms_per_step": v[0] / args.steps} for n, v in sorted(kernels.items(), key=lambda kv: -kv[1][0])}
-    roof = None
-    mfma_kernels = [n for n in ktab if kernel_flops(n, R, N, 64, args.fine, 4) > 0]
-    if mfma_kernels:
-        dom = max(mfma_kernels, key=lambda n: ktab[n]["ms_per_step"])
-        fl = kernel_flops(dom, R, N, 64, args.fine, 4)
-        achieved = fl / (ktab[dom]["ms_per_launch"] * 1e-3) / 1e12
-        roof = {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F16_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK_F16_TFLOPS, 4), "traffic": None,
-                "flops_per_launch": fl}
-        for n in ktab:
-            f = kernel_flops(n, R, N, 64, args.fine, 4)
-            if f:
-                ktab[n]["tflops"] = round(f / (ktab[n]["ms_per_launch"] * 1e-3) / 1e12, 2)
+    ktab, roof = kernel_table(prof, args.steps, R, N, args.fine)
 
     step_ms = elapsed / args.steps * 1e3
     value = R * world * args.steps / elapsed

@@ -10,6 +10,9 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmli_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 SOURCES = ["rays.hip", "sdf.hip", "mlp.hip", "wgrad.hip", "params.hip"]
+# sdf.hip: no SLP packing, so fma(fp16 -> fp32 feature, w, acc) selects v_fma_mix_f32 (one
+# instruction) instead of v_cvt_f32_f16 x2 + v_pk_fma_f32
+PER_FILE = {"sdf.hip": ["-fno-slp-vectorize"]}
 FLAGS = ["-O3", "--offload-arch=gfx950", "-fPIC", "-std=c++17", "-ffp-contract=off",
          "-I", os.path.join(REPO, "include"), "-I", CSRC]
 
@@ -17,7 +20,7 @@ FLAGS = ["-O3", "--offload-arch=gfx950", "-fPIC", "-std=c++17", "-ffp-contract=o
 def _compile(src, extra, tag=""):
     obj = os.path.join(CSRC, "build" + tag, os.path.splitext(src)[0] + ".o")
     os.makedirs(os.path.dirname(obj), exist_ok=True)
-    cmd = [HIPCC] + FLAGS + list(extra) + ["-c", os.path.join(CSRC, src), "-o", obj]
+    cmd = [HIPCC] + FLAGS + PER_FILE.get(src, []) + list(extra) + ["-c", os.path.join(CSRC, src), "-o", obj]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError("hipcc failed for %s:\n%s" % (src, res.stderr))

@@ -39,9 +39,12 @@ MLI_FI half8 acc_to_frag(const f32x16& v, int s) {
 }
 
 MLI_FI float softplus100(float x) {
-  // torch.nn.functional.softplus(x, beta=100, threshold=20) with hardware exp/log.
+  // torch.nn.functional.softplus(x, beta=100, threshold=20) on the raw v_exp_f32 / v_log_f32
+  // (base 2; the log argument 1 + e^t >= 1 is never denormal, so the denormal-scaling
+  // expansion of logf is dead weight): log(1 + e^t) / 100 = log2(1 + 2^(t log2 e)) * ln2/100.
   const float t = x * 100.0f;
-  const float sp = __logf(1.0f + __expf(t)) * 0.01f;
+  const float e = __builtin_amdgcn_exp2f(t * 1.4426950408889634f);
+  const float sp = __builtin_amdgcn_logf(1.0f + e) * 0.0069314718055994531f;
   return t > 20.0f ? x : sp;
 }
 

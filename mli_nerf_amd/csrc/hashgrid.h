@@ -37,32 +37,46 @@ MLI_FI void hash_level(const uint16_t* __restrict__ table, const LevelP& P, floa
   const bool dense_lane = (uint64_t)P.res * P.res * P.res <= (uint64_t)P.size;
 #pragma unroll
   for (int f = 0; f < 8; ++f) acc[f] = 0.0f;
+  auto corners = [&](auto index_of) MLI_LAMBDA_FI {
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const uint32_t cx = g[0] + (c & 1), cy = g[1] + ((c >> 1) & 1), cz = g[2] + ((c >> 2) & 1);
-    float w = 1.0f;
-    w *= (c & 1) ? pos[0] : 1.0f - pos[0];
-    w *= ((c >> 1) & 1) ? pos[1] : 1.0f - pos[1];
-    w *= ((c >> 2) & 1) ? pos[2] : 1.0f - pos[2];
-    uint32_t idx;
-    if (KIND == 0) {
-      idx = fastmod_u32(cx + cy * P.res + cz * r2, P.magic, P.size);
-    } else if (KIND == 1) {
-      idx = (cx ^ (cy * 2654435761u) ^ (cz * 805459861u)) & (P.size - 1u);
-    } else {
-      const uint32_t id = fastmod_u32(cx + cy * P.res + cz * r2, P.magic, P.size);
-      const uint32_t ih = (cx ^ (cy * 2654435761u) ^ (cz * 805459861u)) & (P.size - 1u);
-      idx = dense_lane ? id : ih;
-    }
-    const u32x4 raw = *reinterpret_cast<const u32x4*>(table + (size_t)(P.offset + idx) * 8);
-    const uint32_t words[4] = {raw[0], raw[1], raw[2], raw[3]};
+    for (int c = 0; c < 8; ++c) {
+      const uint32_t cx = g[0] + (c & 1), cy = g[1] + ((c >> 1) & 1), cz = g[2] + ((c >> 2) & 1);
+      float w = 1.0f;
+      w *= (c & 1) ? pos[0] : 1.0f - pos[0];
+      w *= ((c >> 1) & 1) ? pos[1] : 1.0f - pos[1];
+      w *= ((c >> 2) & 1) ? pos[2] : 1.0f - pos[2];
+      const uint32_t idx = index_of(cx, cy, cz);
+      const u32x4 raw = *reinterpret_cast<const u32x4*>(table + (size_t)(P.offset + idx) * 8);
+      const uint32_t words[4] = {raw[0], raw[1], raw[2], raw[3]};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f16 lo = __builtin_bit_cast(f16, (uint16_t)(words[q] & 0xFFFFu));
-      const f16 hi = __builtin_bit_cast(f16, (uint16_t)(words[q] >> 16));
-      acc[2 * q] = fmaf(w, (float)lo, acc[2 * q]);
-      acc[2 * q + 1] = fmaf(w, (float)hi, acc[2 * q + 1]);
+      for (int q = 0; q < 4; ++q) {
+        const f16 lo = __builtin_bit_cast(f16, (uint16_t)(words[q] & 0xFFFFu));
+        const f16 hi = __builtin_bit_cast(f16, (uint16_t)(words[q] >> 16));
+        acc[2 * q] = fmaf(w, (float)lo, acc[2 * q]);
+        acc[2 * q + 1] = fmaf(w, (float)hi, acc[2 * q + 1]);
+      }
     }
+  };
+  auto dense_mod = [&](uint32_t cx, uint32_t cy, uint32_t cz) MLI_LAMBDA_FI {
+    return fastmod_u32(cx + cy * P.res + cz * r2, P.magic, P.size);
+  };
+  auto hashed = [&](uint32_t cx, uint32_t cy, uint32_t cz) MLI_LAMBDA_FI {
+    return (cx ^ (cy * 2654435761u) ^ (cz * 805459861u)) & (P.size - 1u);
+  };
+  if (KIND == 0) {
+    // whole cell inside the dense grid (every corner index < res^3 <= size): the modulo is
+    // the identity -- a uniform branch skips the 64-bit fastmod when the whole wave qualifies
+    const bool in_grid = g[0] + 1 < P.res && g[1] + 1 < P.res && g[2] + 1 < P.res;
+    if (__all(in_grid))
+      corners([&](uint32_t cx, uint32_t cy, uint32_t cz) MLI_LAMBDA_FI { return cx + cy * P.res + cz * r2; });
+    else
+      corners(dense_mod);
+  } else if (KIND == 1) {
+    corners(hashed);
+  } else {
+    corners([&](uint32_t cx, uint32_t cy, uint32_t cz) MLI_LAMBDA_FI {
+      return dense_lane ? dense_mod(cx, cy, cz) : hashed(cx, cy, cz);
+    });
   }
 }
 

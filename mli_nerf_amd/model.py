@@ -248,22 +248,40 @@ class Model(torch.nn.Module):
         return out
 
     @torch.no_grad()
-    def inference(self, data):
-        """NeuralLumen/model.py:60-111: full image in rand_rays_val chunks, eval branch."""
+    def inference(self, data, shard=True):
+        """NeuralLumen/model.py:60-111: full image in rand_rays_val chunks, eval branch.
+
+        Under an initialised process group with world > 1 (and shard=True) each rank renders
+        one contiguous tile of the frame and ONE all_gather assembles it, so
+        every rank returns the full maps."""
+        from . import shard as sh
         self.eval()
         self.prepare()
         H, W = self.image_size_val
         n_pix = H * W
         self.image_width = W
-        chunks = []
-        for start in range(0, n_pix, self.rand_rays_val):
-            R = min(self.rand_rays_val, n_pix - start)
-            ridx = torch.arange(start, start + R, device=self.flat.device)[None]
+        world, rank, group = 1, 0, None
+        if shard:
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+                world, rank = dist.get_world_size(), dist.get_rank()
+        lo, hi, _ = sh.shard_range(n_pix, rank, world)
+        # mli_rgb_fwd takes whole 256-sample workgroups: pad each chunk's ray count so
+        # R * N % 256 == 0 (repeating the last pixel), drop the padding afterwards
+        N = self.pcfg.n_samples
+        step = 256 // math.gcd(N, 256)
+        dev = self.flat.device
+        parts = []
+        for start in range(lo, hi, self.rand_rays_val):
+            R = min(self.rand_rays_val, hi - start)
+            Rp = -(-R // step) * step
+            ridx = torch.arange(start, start + Rp, device=dev).clamp_(max=start + R - 1)[None]
             d = dict(pose=data["pose"], intr=data["intr"], pose_light=data["pose_light"], ray_idx=ridx)
             st = self.engine.render(d, self.s_var.detach(), self.progress, False, u=None, W=W)
-            comp = st[4]
-            chunks.append({k: comp[k].clone() for k in ("rgb", "o_r", "o_s", "o_re", "opacity", "gradient", "depth")})
-        out = {k: torch.cat([c[k] for c in chunks], 0)[None] for k in chunks[0]}
+            parts.append(sh.pack(st[4])[:R])
+        local = torch.cat(parts, 0) if parts else torch.zeros(0, sh.N_CHANNELS, device=dev)
+        packed = sh.gather_tiles(local, n_pix, world, group) if world > 1 else local
+        out = {k: v.contiguous()[None] for k, v in sh.unpack(packed).items()}
         rot = data["pose"][..., :3, :3]
         normal_cam = -out["gradient"] @ rot.transpose(-1, -2)
 

@@ -14,7 +14,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from mli_nerf_amd import layout
+from mli_nerf_amd import layout, shard
 from mli_nerf_amd.trainer import reduce_gradients
 
 WORLD = 2
@@ -74,3 +74,41 @@ def test_single_rank_is_identity():
     g = torch.randn(10)
     h = g.clone()
     assert reduce_gradients(h, 1) is h and torch.equal(h, g)
+
+
+def _tile_worker(rank, port, results, n):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        lo, hi, _ = shard.shard_range(n, rank, WORLD)
+        # each ray's 15 channels = a function of its pixel index (stands in for the render)
+        pix = torch.arange(lo, hi, dtype=torch.float32)[:, None]
+        local = pix * 100 + torch.arange(shard.N_CHANNELS, dtype=torch.float32)[None]
+        results[rank] = shard.gather_tiles(local, n, WORLD)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("n", [640, 641])
+def test_inference_tiles_gather_world2(n):
+    """config 5 sharding: contiguous tiles per rank, ONE all_gather rebuilds the frame
+    (uneven n: the last tile is padded and the padding dropped)."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    results = ctx.Manager().dict()
+    mp.start_processes(_tile_worker, args=(port, results, n), nprocs=WORLD, join=True, start_method="spawn")
+    full = torch.arange(n, dtype=torch.float32)[:, None] * 100 + torch.arange(shard.N_CHANNELS)[None]
+    for r in range(WORLD):
+        assert torch.equal(results[r], full)
+
+
+def test_shard_ranges_cover_frame():
+    for n, world in [(640000, 8), (97, 8), (5, 8), (10, 1)]:
+        spans = [shard.shard_range(n, r, world)[:2] for r in range(world)]
+        assert spans[0][0] == 0 and spans[-1][1] == n
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+        packed = torch.randn(7, shard.N_CHANNELS)
+        back = shard.pack(shard.unpack(packed))
+        assert torch.equal(back, packed)

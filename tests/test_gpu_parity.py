@@ -245,3 +245,30 @@ def _gpu_total(out, data, pcfg):
     from mli_nerf_amd.trainer import stage_b_losses
     total, _, _ = stage_b_losses(out, data, pcfg.loss_w, pcfg.intrinsic_ranges, pcfg.re_factors)
     return total
+
+
+def test_inference_full_image():
+    """Model.inference (NeuralLumen/model.py:60-111): the whole val image in rand_rays_val
+    chunks (an odd chunk size, so the last chunk is padded to whole 256-sample workgroups),
+    eval branch (u = 0.5 midpoints, no hessian), against the oracle's eval forward on every
+    pixel.  Free-running (the eval sampler is deterministic but chaotic like training):
+    mean abs 2e-3, max 0.1, PSNR of the difference >= 40 dB."""
+    _need_gpu()
+    model, sd, data, pcfg, (Hh, W) = build("syn_hotdog_b", 64, 16, 4, 4, 14, 3.0)
+    Hv, Wv = 18, 24
+    model.image_size_val = [Hv, Wv]
+    model.rand_rays_val = 203
+    out = model.inference(to_dev(data))
+    assert out["rgb_map"].shape == (1, 3, Hv, Wv) and out["normal_map"].shape == (1, 3, Hv, Wv)
+    full = dict(data)
+    full["ray_idx"] = torch.arange(Hv * Wv)[None]
+    with torch.no_grad():
+        ref = o_render.forward(fp16_table_sd(sd), pcfg, full, u=None, training=False, progress=0.0,
+                               width=Wv, height=Hv)
+    for key in ("rgb", "o_r", "o_s", "o_re", "opacity"):
+        d = (out[key].cpu().reshape(ref[key].shape) - ref[key]).abs()
+        psnr_d = -10 * math.log10(max(float((d ** 2).mean()), 1e-20))
+        print("inference %s max %.3g mean %.3g psnr(diff) %.1f dB" % (key, d.max(), d.mean(), psnr_d))
+        assert d.max() < 0.1 and d.mean() < 2e-3 and psnr_d > 40, key
+    # the maps are the per-ray outputs laid out [B, C, H, W]
+    torch.testing.assert_close(out["rgb_map"][0].permute(1, 2, 0).reshape(-1, 3), out["rgb"][0])
