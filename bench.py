@@ -55,6 +55,27 @@ def kernel_flops(name, R, N, Nc, Nf, H):
     return 0
 
 
+PMC_SUMMARY = os.path.join(HERE, "profiles", "r1", "pmc_summary.json")
+PMC_SAMPLES = 4096 * 128  # the workload the committed PMC passes ran (tools/pmc.sh: bench.py defaults)
+
+
+def pmc_traffic(kernel, n_units_check):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary
+    (tools/pmc.sh + tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md
+    §HBM corrections), when it was collected on this same workload."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            summ = json.load(f)
+    except OSError:
+        return None
+    rec = summ.get(kernel)
+    if rec is None or n_units_check != PMC_SAMPLES:
+        return None
+    return {"traffic": round(rec["hbm_bytes"]), "traffic_read": round(rec["hbm_read_bytes"]),
+            "traffic_write": round(rec["hbm_write_bytes"]),
+            "traffic_source": os.path.relpath(PMC_SUMMARY, HERE) + " (rocprofv3 --pmc, separate passes)"}
+
+
 def kernel_table(prof, n_units, R, N, fine):
     """Per-call-name HIP-event timings -> table + roofline record of the dominant MFMA call."""
     kernels = {}
@@ -73,6 +94,9 @@ def kernel_table(prof, n_units, R, N, fine):
         roof = {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_F16_TFLOPS, 4), "traffic": None,
                 "flops_per_launch": fl}
+        pmc = pmc_traffic(dom, n_units_check=R * N)
+        if pmc:
+            roof.update(pmc)
         for n in ktab:
             f = kernel_flops(n, R, N, 64, fine, 4)
             if f:
@@ -147,7 +171,7 @@ def run_infer(args, world, rank, dev):
         torch.set_num_threads(threads)
         sd = synthetic.make_state_dict(log2T=22, seed=0)
         pcfg = o_render.PathCfg(n_fine=args.fine)
-        data = {k: v.cpu() for k, v in frames[args.warmup].items()}
+        data = {k: v.cpu() for k, v in frames[-1].items()}  # the last rendered frame is `out`
         n_cpu = args.cpu_rays * 4
         data["ray_idx"] = torch.arange(n_cpu)[None] * (n_pix // n_cpu)
         with torch.no_grad():

@@ -69,6 +69,9 @@ def _corner_index(gx, gy, gz, res, size):
     return index % size
 
 
+_CORNER_BITS = torch.tensor([[(c >> d) & 1 for d in range(3)] for c in range(8)], dtype=torch.int64)
+
+
 def encode(x01, params, table, n_feat=8):
     """x01 [n,3] float32 in (roughly) [0,1]; params flat float32 -> [n, L*n_feat] float32."""
     x01 = x01.to(torch.float32)
@@ -83,16 +86,16 @@ def encode(x01, params, table, n_feat=8):
         frac = pos - g
         gi = g.to(torch.int64) & MASK32  # (uint32_t)(int) conversion
         acc = torch.zeros(n, n_feat, dtype=torch.float32)
+        # uint32 corner indices of all 8 corners at once (integer math: order-free); the
+        # float weights and the accumulation keep the per-corner order c = 0..7
+        gc = (gi[:, None, :] + _CORNER_BITS[None]) & MASK32
+        idx8 = _corner_index(gc[..., 0], gc[..., 1], gc[..., 2], res, size)
         for c in range(8):
             bits = [(c >> d) & 1 for d in range(3)]
             w = torch.ones(n, dtype=torch.float32)
             for d in range(3):
                 w = w * (frac[:, d] if bits[d] else (1.0 - frac[:, d]))
-            gx = (gi[:, 0] + bits[0]) & MASK32
-            gy = (gi[:, 1] + bits[1]) & MASK32
-            gz = (gi[:, 2] + bits[2]) & MASK32
-            idx = _corner_index(gx, gy, gz, res, size)
-            acc = acc + w[:, None] * grid[offset + idx]
+            acc = acc + w[:, None] * grid[offset + idx8[:, c]]
         outs.append(acc)
     return torch.cat(outs, dim=-1)
 
