@@ -35,7 +35,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mli_stream_t; /* == hipStream_t */
 
-#define MLI_ABI_VERSION 2
+#define MLI_ABI_VERSION 5
 #define MLI_HIDDEN 256
 #define MLI_LEVELS 16
 #define MLI_LEVEL_FEAT 8
@@ -59,9 +59,9 @@ const char* mli_error_string(int code);
  * F.normalize (NeuralLumen/model.py:125) and get_dist_bounds (neuralangelo/model.py:420-430,
  * nerf_util.py:199-205, NeuralLumen/utils/utils.py:86-123).  Only the R sampled rays are built. */
 typedef struct {
-  const float* intr_inv;  /* [3,3] inverse intrinsics (host: intr.inverse())            */
-  const float* c2w;       /* [3,4] Pose.invert(pose)                                      */
-  const float* c2w_light; /* [3,4] Pose.invert(pose_light)                                */
+  const float* intr;      /* [3,3] intrinsics (inverted in-kernel, camera.py:259)          */
+  const float* pose;      /* [3,4] world-to-camera [R|t] (Pose.invert in-kernel, camera.py:46-52) */
+  const float* pose_light; /* [3,4] world-to-light; pts_light = its camera center          */
   const int64_t* ray_idx; /* [R] flat pixel index y*W + x (NULL: ray r = pixel first+r)   */
   int64_t first_pixel;    /* used when ray_idx == NULL (full-image chunks)                */
   int R, W;
@@ -117,6 +117,8 @@ typedef struct {
   float* grad;            /* [n_per_ray][R][3] (FIELD) */
   float* hess;            /* [n_per_ray][R][3] (FIELD, with_hessian) */
   uint16_t* h0;           /* frag image [S/32][16][64][8] (FIELD) */
+  uint16_t* enc;          /* FIELD scratch: hash encodings of the 5 points (center + 4 taps)
+                             as MFMA B-fragment images [S/32][5][8][64][8] fp16 (S*640 halves) */
 } mli_sdf_args;
 int mli_sdf(const mli_sdf_args* a, mli_stream_t s);
 
@@ -233,6 +235,28 @@ typedef struct {
   int classes;            /* MLI_WGRAD_* mask */
 } mli_wgrad_args;
 int mli_wgrad(const mli_wgrad_args* a, mli_stream_t s);
+
+/* ---------------------------------------------------------------- losses
+ * Stage-b loss terms and d(total)/d(rgb, o_r, o_s, o_re) in one call (three launches):
+ * replaces NeuralLumen/trainer.py:133-149 (_compute_loss) with eikonal/curvature
+ * (neuralangelo/utils/misc.py:74-90), intrinsic_loss / regularize_re_loss
+ * (NeuralLumen/utils/utils.py:142-174) and _get_total_loss (imaginaire/trainers/base.py:534-544).
+ * Gradients are deterministic; loss values are fp32 atomic sums (logging). */
+typedef struct {
+  int R, N;
+  const float* rgb; const float* o_r; const float* o_s; const float* o_re; /* [R,3],[R,3],[R],[R,3] */
+  const float* gt;        /* image_sampled [R,3] */
+  const float* ref; const float* sha; const float* cert; /* pseudo labels [R,3],[R],[R] (NULL: intrinsic off) */
+  const uint8_t* outside; /* [R] */
+  const float* grad; const float* hess; /* [N][R][3] (NULL skips eikonal / curvature) */
+  float w_render, w_eikonal, w_curvature, w_intrinsic, w_re;
+  float range_sha_lo, range_sha_hi, range_vis_lo, range_vis_hi, f_ref, f_sha;
+  float f_neg, f_pos, e_pos;
+  float* d_rgb; float* d_o_r; float* d_o_s; float* d_o_re; /* d total / d output */
+  float* losses;          /* [8]: render, eikonal, curvature, intrinsic, regularize_re, total, psnr, mse */
+  float* scratch;         /* [12] device, zeroed once by the caller (left zeroed by every call) */
+} mli_loss_args;
+int mli_stage_b_loss(const mli_loss_args* a, mli_stream_t s);
 
 /* ---------------------------------------------------------------- parameters
  * Weight-norm W = g * v / ||v||_row (torch.nn.utils.weight_norm dim=0) folded once per

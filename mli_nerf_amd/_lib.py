@@ -19,7 +19,7 @@ class GridLevels(C.Structure):
 
 
 class RaysArgs(C.Structure):
-    _fields_ = [("intr_inv", P), ("c2w", P), ("c2w_light", P), ("ray_idx", P), ("first_pixel", I64),
+    _fields_ = [("intr", P), ("pose", P), ("pose_light", P), ("ray_idx", P), ("first_pixel", I64),
                 ("R", I32), ("W", I32), ("bounding", I32), ("aabb", F32 * 6),
                 ("center", P), ("ray_unit", P), ("ray_norm", P), ("pts_light", P),
                 ("near_", P), ("far_", P), ("outside", P)]
@@ -33,7 +33,8 @@ class SdfArgs(C.Structure):
     _fields_ = [("mode", I32), ("R", I32), ("n_per_ray", I32), ("center", P), ("ray_unit", P),
                 ("dists", P), ("outside", P), ("table", P), ("levels", GridLevels), ("wsdf", P),
                 ("eps", F32), ("grad_den", F32), ("hess_den", F32), ("outside_val", F32),
-                ("with_hessian", I32), ("sdf", P), ("grad", P), ("hess", P), ("h0", P)]
+                ("with_hessian", I32), ("sdf", P), ("grad", P), ("hess", P), ("h0", P),
+                ("enc", P)]
 
 
 class SampleCoarseArgs(C.Structure):
@@ -78,6 +79,16 @@ class WgradArgs(C.Structure):
     _fields_ = [("S", I32), ("n_jobs", I32), ("jobs", P), ("classes", I32)]
 
 
+class LossArgs(C.Structure):
+    _fields_ = [("R", I32), ("N", I32), ("rgb", P), ("o_r", P), ("o_s", P), ("o_re", P), ("gt", P),
+                ("ref", P), ("sha", P), ("cert", P), ("outside", P), ("grad", P), ("hess", P),
+                ("w_render", F32), ("w_eikonal", F32), ("w_curvature", F32), ("w_intrinsic", F32),
+                ("w_re", F32), ("range_sha_lo", F32), ("range_sha_hi", F32), ("range_vis_lo", F32),
+                ("range_vis_hi", F32), ("f_ref", F32), ("f_sha", F32), ("f_neg", F32), ("f_pos", F32),
+                ("e_pos", F32), ("d_rgb", P), ("d_o_r", P), ("d_o_s", P), ("d_o_re", P), ("losses", P),
+                ("scratch", P)]
+
+
 class PackLayer(C.Structure):
     _fields_ = [("v", P), ("g", P), ("bias", P), ("n_out", I32), ("k_ref", I32), ("transpose", I32),
                 ("n_tiles", I32), ("k_steps", I32), ("kmap", P), ("kmode", P), ("dst_offset", I64),
@@ -111,7 +122,7 @@ class CastArgs(C.Structure):
     _fields_ = [("src", P), ("dst", P), ("n", I64)]
 
 
-ABI_VERSION = 2  # include/mli_hip.h MLI_ABI_VERSION
+ABI_VERSION = 5  # include/mli_hip.h MLI_ABI_VERSION
 
 ENTRY_POINTS = {
     "mli_rays": RaysArgs, "mli_hashgrid_fwd": HashgridArgs, "mli_sdf": SdfArgs,
@@ -119,7 +130,7 @@ ENTRY_POINTS = {
     "mli_rgb_fwd": RgbFwdArgs, "mli_composite_fwd": CompositeArgs,
     "mli_composite_bwd": CompositeBwdArgs, "mli_rgb_bwd": RgbBwdArgs, "mli_wgrad": WgradArgs,
     "mli_pack": PackArgs, "mli_pack_sdf": PackSdfArgs, "mli_grad_assemble": AssembleArgs,
-    "mli_adamw": AdamwArgs, "mli_cast_f16": CastArgs,
+    "mli_adamw": AdamwArgs, "mli_cast_f16": CastArgs, "mli_stage_b_loss": LossArgs,
 }
 
 _lib = None

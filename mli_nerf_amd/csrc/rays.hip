@@ -16,8 +16,25 @@ __global__ __launch_bounds__(256) void rays_kernel(mli_rays_args a) {
   const int64_t pix = a.ray_idx ? a.ray_idx[r] : a.first_pixel + r;
   const float py = (float)(pix / a.W) + 0.5f;
   const float px = (float)(pix % a.W) + 0.5f;
-  const float* K = a.intr_inv;
-  const float* T = a.c2w;
+  // intr.inverse() (camera.py:259) by the adjugate, and Pose.invert (camera.py:46-52):
+  // c2w = [R^T | -R^T t], recomputed per thread (a few dozen flops, no host round trip)
+  float K[9], T[12], TL[3];
+  {
+    const float* M = a.intr;
+    const float c00 = M[4] * M[8] - M[5] * M[7], c01 = M[5] * M[6] - M[3] * M[8], c02 = M[3] * M[7] - M[4] * M[6];
+    const float det = (M[0] * c00 + M[1] * c01) + M[2] * c02;
+    const float id = 1.0f / det;
+    K[0] = c00 * id; K[1] = (M[2] * M[7] - M[1] * M[8]) * id; K[2] = (M[1] * M[5] - M[2] * M[4]) * id;
+    K[3] = c01 * id; K[4] = (M[0] * M[8] - M[2] * M[6]) * id; K[5] = (M[2] * M[3] - M[0] * M[5]) * id;
+    K[6] = c02 * id; K[7] = (M[1] * M[6] - M[0] * M[7]) * id; K[8] = (M[0] * M[4] - M[1] * M[3]) * id;
+    const float* P = a.pose;  // w2c [R | t]
+    for (int i = 0; i < 3; ++i) {
+      for (int j = 0; j < 3; ++j) T[4 * i + j] = P[4 * j + i];
+      T[4 * i + 3] = -((P[4 * 0 + i] * P[3] + P[4 * 1 + i] * P[7]) + P[4 * 2 + i] * P[11]);
+    }
+    const float* Q = a.pose_light;
+    for (int i = 0; i < 3; ++i) TL[i] = -((Q[4 * 0 + i] * Q[3] + Q[4 * 1 + i] * Q[7]) + Q[4 * 2 + i] * Q[11]);
+  }
   // img2cam: [px, py, 1] @ Kinv^T   (camera.py:259-260)
   float cam[3];
   for (int i = 0; i < 3; ++i) cam[i] = (px * K[3 * i + 0] + py * K[3 * i + 1]) + K[3 * i + 2];
@@ -35,7 +52,7 @@ __global__ __launch_bounds__(256) void rays_kernel(mli_rays_args a) {
     c[i] = T[4 * i + 3];
     a.center[3 * r + i] = c[i];
     a.ray_unit[3 * r + i] = v[i];
-    a.pts_light[3 * r + i] = a.c2w_light[4 * i + 3];
+    a.pts_light[3 * r + i] = TL[i];
   }
   a.ray_norm[r] = nrm;
   float nr, fr;

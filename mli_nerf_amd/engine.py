@@ -134,10 +134,8 @@ class RenderEngine:
     # ------------------------------------------------------------------ forward
     @torch.no_grad()
     def rays(self, pose, intr, pose_light, ray_idx, W, R=None, first_pixel=0):
-        """pose/intr/pose_light [1,3,4]/[1,3,3]/[1,3,4]; ray_idx [1,R] int64 or None."""
-        c2w = _invert(pose[0]).contiguous()
-        c2w_l = _invert(pose_light[0]).contiguous()
-        kinv = intr[0].inverse().contiguous()
+        """pose/intr/pose_light [1,3,4]/[1,3,3]/[1,3,4] (inverted in-kernel); ray_idx [1,R] int64 or None."""
+        w2c, w2l, K = pose[0].contiguous(), pose_light[0].contiguous(), intr[0].contiguous()
         R = R if ray_idx is None else ray_idx.shape[-1]
         ridx = None if ray_idx is None else ray_idx.reshape(-1).to(torch.int64).contiguous()
         out = dict(center=self._buf("center", (R, 3)), ray_unit=self._buf("ray_unit", (R, 3)),
@@ -145,21 +143,25 @@ class RenderEngine:
                    near=self._buf("near", (R,)), far=self._buf("far", (R,)),
                    outside=self._buf("outside", (R,), torch.uint8))
         aabb = (C.c_float * 6)(*self.cfg.aabb)
-        L.call("mli_rays", L.RaysArgs(L.ptr(kinv), L.ptr(c2w), L.ptr(c2w_l), L.ptr(ridx), first_pixel, R, W,
+        L.call("mli_rays", L.RaysArgs(L.ptr(K), L.ptr(w2c), L.ptr(w2l), L.ptr(ridx), first_pixel, R, W,
                                       1 if self.cfg.bounding == "box" else 0, aabb,
                                       L.ptr(out["center"]), L.ptr(out["ray_unit"]), L.ptr(out["ray_norm"]),
                                       L.ptr(out["pts_light"]), L.ptr(out["near"]), L.ptr(out["far"]),
                                       L.ptr(out["outside"])))
-        out["_keep"] = (c2w, c2w_l, kinv, ridx)
+        out["_keep"] = (w2c, w2l, K, ridx)
         return out
 
     def _sdf(self, rays, dists, n_per_ray, out, mode=0, grad=None, hess=None, h0=None):
         R = rays["center"].shape[0]
+        enc = None
+        if mode == 1:
+            tiles = (R * n_per_ray + 31) // 32
+            enc = self._buf("enc5", (tiles * 32 * 640,), torch.float16)
         L.call("mli_sdf", L.SdfArgs(mode, R, n_per_ray, L.ptr(rays["center"]), L.ptr(rays["ray_unit"]),
                                     L.ptr(dists), L.ptr(rays["outside"]), L.ptr(self.table16), self.levels,
                                     L.ptr(self.wsdf), self.eps, self.grad_den, self.hess_den,
                                     self.cfg.outside_val, 1 if hess is not None else 0, L.ptr(out),
-                                    L.ptr(grad), L.ptr(hess), L.ptr(h0)))
+                                    L.ptr(grad), L.ptr(hess), L.ptr(h0), L.ptr(enc)))
 
     @torch.no_grad()
     def sample(self, rays, u=None):
@@ -327,9 +329,3 @@ class RenderEngine:
         L.call("mli_grad_assemble", L.AssembleArgs(15, L.ptr(ad), 1.0 / scale))
         return grad_out
 
-
-def _invert(pose):
-    """camera.Pose.invert (projects/nerf/utils/camera.py:46-52) on a [3,4] tensor."""
-    rot, trans = pose[:, :3], pose[:, 3:]
-    rt = rot.transpose(0, 1)
-    return torch.cat([rt, -(rt @ trans)], dim=1)

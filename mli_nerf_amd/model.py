@@ -225,14 +225,24 @@ class Model(torch.nn.Module):
         """NeuralLumen/model.py:113-118 -> render_pixels_lumen; ``u`` injects the stratified
         uniforms (nerf_util.py:33) for parity runs."""
         self.prepare()
-        stratified = self.stratified and self.training
-        if stratified and u is None:
-            u = torch.rand(1, data["ray_idx"].shape[-1], self.pcfg.n_coarse, device=self.flat.device)
-        if not stratified:
-            u = None
+        u = self.stratified_uniforms(data, u)
         self.image_width = self.image_size_train[1]
         rgb, o_r, o_s, o_re = _RenderHeads.apply(self.flat, self, data, u, self.progress, self.training)
-        rays, dists, fld, hd, comp = self._last_state
+        return self.outputs(self._last_state, (rgb, o_r, o_s, o_re))
+
+    def stratified_uniforms(self, data, u=None):
+        """nerf_util.py:33: U[0,1) per coarse bin in training, midpoints (None) in eval."""
+        if not (self.stratified and self.training):
+            return None
+        if u is None:
+            u = torch.rand(1, data["ray_idx"].shape[-1], self.pcfg.n_coarse, device=self.flat.device)
+        return u
+
+    def outputs(self, st, heads=None):
+        """The reference output dict (NeuralLumen/model.py:312-323) of a render state; ``heads``
+        = differentiable (rgb, o_r, o_s, o_re) when called under autograd."""
+        rays, dists, fld, hd, comp = st
+        rgb, o_r, o_s, o_re = heads if heads is not None else (comp["rgb"], comp["o_r"], comp["o_s"], comp["o_re"])
         N, R = dists.shape
         out = dict(rgb=rgb[None], o_r=o_r[None], o_s=o_s[None], o_re=o_re[None],
                    outside=rays["outside"].bool().view(1, R, 1),

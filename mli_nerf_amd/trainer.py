@@ -52,7 +52,16 @@ def curvature_loss(hessians, outside):
     return (lap * (~outside).float()).mean()
 
 
-def stage_b_losses(out, data, weights, ranges=((0.0, 1.0), (0.0, 1.0)), re_factors=(10.0, 1.0, 1.0)):
+FUSED_LOSSES = {"render", "eikonal", "curvature", "intrinsic", "regularize_re"}
+LOSS_NAMES = ("render", "eikonal", "curvature", "intrinsic", "regularize_re")
+
+
+def _c(t):
+    return None if t is None else t.contiguous()
+
+
+def stage_b_losses(out, data, weights, ranges=((0.0, 1.0), (0.0, 1.0)), re_factors=(10.0, 1.0, 1.0),
+                   intr_factors=(1.0, 1.0)):
     losses = {}
     if "render" in weights:
         losses["render"] = F.l1_loss(out["rgb"], data["image_sampled"]) * 3
@@ -63,7 +72,7 @@ def stage_b_losses(out, data, weights, ranges=((0.0, 1.0), (0.0, 1.0)), re_facto
     if "intrinsic" in weights:
         losses["intrinsic"] = intrinsic_loss(out["o_r"], out["o_s"], data["pseudo_ref_sampled"],
                                              data["pseudo_sha_sampled"],
-                                             data["pseudo_visibility_certainty_sampled"], ranges)
+                                             data["pseudo_visibility_certainty_sampled"], ranges, intr_factors)
     if "regularize_re" in weights:
         losses["regularize_re"] = regularize_re_loss(out["o_re"], *re_factors)
     total = sum(losses[k] * weights[k] for k in weights if k in losses)
@@ -129,8 +138,10 @@ class Trainer:
         self.weights = {k: v for k, v in cfg.trainer.loss_weight.items() if v}
         p = cfg.trainer.para_intrinsic_loss
         self.ranges = (tuple(p["weight_map_range_shading"]), tuple(p["weight_map_range_visibility"]))
+        self.intr_factors = (float(p.get("factor_ref", 1.0)), float(p.get("factor_sha", 1.0)))
         q = cfg.trainer.para_regularize_re_loss
         self.re_factors = (q["factor_negative"], q["factor_positive"], q["exponent_positive"])
+        self._scratch = self._grad = None
         o = cfg.optim
         self.optim = FusedAdamW(model.flat, lr=o.params.lr, weight_decay=o.params.weight_decay)
         self.sched = o.sched
@@ -149,13 +160,63 @@ class Trainer:
         self.model.progress = self.current_iteration / self.cfg.max_iter
         self.model.neural_sdf.set_normal_epsilon()
 
-    def train_step(self, data, u=None):
+    def train_step(self, data, u=None, return_outputs=False):
+        """One stage-b iteration.  Hot path: render -> fused losses + output gradients
+        (mli_stage_b_loss) -> heads backward -> all-reduce -> fused AdamW, no torch autograd.
+        Loss configurations the fused kernel does not cover take the autograd path (the
+        reference's loss code on Model.forward's outputs)."""
+        self._start_of_iteration()
+        self.model.train()
+        if not set(self.weights) <= FUSED_LOSSES:
+            return self.train_step_autograd(data, u)
+        m = self.model
+        m.prepare()
+        m.image_width = m.image_size_train[1]
+        st = m.engine.render(data, m.s_var.detach(), m.progress, True, u=m.stratified_uniforms(data, u),
+                             W=m.image_width)
+        m._last_state = st
+        eng = m.engine
+        rays, dists, fld, hd, comp = st
+        N, R = dists.shape
+        d_rgb, d_o_r = eng._buf("d_rgb", (R, 3)), eng._buf("d_o_r", (R, 3))
+        d_o_s, d_o_re = eng._buf("d_o_s", (R, 1)), eng._buf("d_o_re", (R, 3))
+        if self._scratch is None or self._scratch.device != m.flat.device:
+            self._scratch = torch.zeros(16, device=m.flat.device)
+        lv = torch.empty(8, device=m.flat.device)
+        w = self.weights
+        intr = "intrinsic" in w
+        L.call("mli_stage_b_loss", L.LossArgs(
+            R, N, L.ptr(comp["rgb"]), L.ptr(comp["o_r"]), L.ptr(comp["o_s"]), L.ptr(comp["o_re"]),
+            L.ptr(_c(data["image_sampled"])), L.ptr(_c(data.get("pseudo_ref_sampled")) if intr else None),
+            L.ptr(_c(data.get("pseudo_sha_sampled")) if intr else None),
+            L.ptr(_c(data.get("pseudo_visibility_certainty_sampled")) if intr else None),
+            L.ptr(rays["outside"]), L.ptr(fld["grad"]) if "eikonal" in w else None,
+            L.ptr(fld["hess"]) if "curvature" in w else None,
+            w.get("render", 0.0), w.get("eikonal", 0.0), w.get("curvature", 0.0), w.get("intrinsic", 0.0),
+            w.get("regularize_re", 0.0), self.ranges[0][0], self.ranges[0][1], self.ranges[1][0],
+            self.ranges[1][1], self.intr_factors[0], self.intr_factors[1], *self.re_factors,
+            L.ptr(d_rgb), L.ptr(d_o_r), L.ptr(d_o_s), L.ptr(d_o_re), L.ptr(lv), L.ptr(self._scratch)))
+        if self._grad is None or self._grad.device != m.flat.device:
+            self._grad = torch.empty_like(m.flat.detach())  # every element is written by the backward
+        grad = eng.backward(st, d_rgb, d_o_r, d_o_s, d_o_re, m.flat, m._sdf_l1(), self._grad)
+        grad = reduce_gradients(grad, self.world_size)
+        m.flat.grad = grad
+        self.optim.step(grad, self.lr())
+        self.current_iteration += 1
+        self.losses = {k: lv[i] for i, k in enumerate(LOSS_NAMES) if k in w}
+        self.losses["total"] = lv[5]
+        self.metrics["psnr"] = lv[6]
+        return m.outputs(st) if return_outputs else None
+
+    def train_step_autograd(self, data, u=None):
+        """Reference semantics through torch autograd on Model.forward's outputs."""
         self._start_of_iteration()
         self.model.train()
         if self.model.flat.grad is not None:
             self.model.flat.grad = None
         out = self.model(data, u=u)
-        total, losses, psnr = stage_b_losses(out, data, self.weights, self.ranges, self.re_factors)
+        total, losses, psnr = stage_b_losses(out, data, self.weights, self.ranges, self.re_factors,
+                                             self.intr_factors)
         total.backward()
         grad = reduce_gradients(self.model.flat.grad, self.world_size)
         self.optim.step(grad, self.lr())

@@ -22,7 +22,7 @@ STRUCTS = {
     "mli_rgb_bwd_args": L.RgbBwdArgs, "mli_wgrad_job": L.WgradJob, "mli_wgrad_args": L.WgradArgs,
     "mli_pack_layer": L.PackLayer, "mli_pack_args": L.PackArgs, "mli_pack_sdf_args": L.PackSdfArgs,
     "mli_assemble_layer": L.AssembleLayer, "mli_assemble_args": L.AssembleArgs,
-    "mli_adamw_args": L.AdamwArgs, "mli_cast_args": L.CastArgs,
+    "mli_adamw_args": L.AdamwArgs, "mli_cast_args": L.CastArgs, "mli_loss_args": L.LossArgs,
 }
 
 

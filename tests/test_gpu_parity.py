@@ -272,3 +272,36 @@ def test_inference_full_image():
         assert d.max() < 0.1 and d.mean() < 2e-3 and psnr_d > 40, key
     # the maps are the per-ray outputs laid out [B, C, H, W]
     torch.testing.assert_close(out["rgb_map"][0].permute(1, 2, 0).reshape(-1, 3), out["rgb"][0])
+
+
+@pytest.mark.parametrize("case", ["hotdog", "pikachu"])
+def test_fused_loss_step_matches_autograd_step(case):
+    """Trainer hot path (mli_stage_b_loss: loss terms + d/d outputs in HIP, no autograd)
+    against the reference-semantics path (torch losses on Model.forward + autograd) on the
+    same render: identical loss terms (1e-5 rel) and identical parameter gradients."""
+    _need_gpu()
+    from mli_nerf_amd.configs import preset as _preset
+    from mli_nerf_amd.trainer import Trainer
+    config = {"hotdog": "syn_hotdog_b", "pikachu": "NRHints_Pikachu_b"}[case]
+    model, sd, data, pcfg, (Hh, W) = build(config, 64, 16, 4, 4, 14, 3.0)
+    cfg = _preset(config, rays=64, n_coarse=16, n_fine=4, log2T=14)
+    u = torch.rand(1, 64, 16).to(DEV)
+    dd = to_dev(data)
+    tr = Trainer(cfg, model)
+    tr.optim.lr = 0.0  # keep the parameters fixed between the two steps
+    tr.optim.wd = 0.0
+    tr.train_step(dd, u=u)
+    fused = {k: float(v) for k, v in tr.losses.items()}
+    g_fused = model.flat.grad.detach().clone()
+    psnr_fused = float(tr.metrics["psnr"])
+    tr.current_iteration = 0
+    tr.train_step_autograd(dd, u=u)
+    auto = {k: float(v) for k, v in tr.losses.items()}
+    g_auto = model.flat.grad.detach().clone()
+    print(case, "fused", fused, "autograd", auto)
+    for k in auto:
+        assert abs(fused[k] - auto[k]) <= 1e-5 * max(1.0, abs(auto[k])), k
+    assert abs(psnr_fused - float(tr.metrics["psnr"])) < 1e-4
+    rel = ((g_fused - g_auto).norm() / g_auto.norm()).item()
+    print(case, "grad rel diff", rel)
+    assert rel < 1e-5
