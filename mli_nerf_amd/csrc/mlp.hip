@@ -34,7 +34,8 @@ constexpr int FRAG_TILE = 16 * 64 * 8;  // halves per 32-sample tile of a 256-wi
 // weight ring: NSLOT slots of 3 x 8 KiB (one 16 B LDS-DMA per thread per 8 KiB round)
 constexpr int GLDS = 3;
 constexpr int SLOT = GLDS * 8192;       // >= CH(19) = 19584
-constexpr int NSLOT = 3;                // DMA distance 2 + the slot being read
+constexpr int DIST = 2;                 // chunks in flight ahead of the one being read
+constexpr int NSLOT = DIST + 1;
 // feature-major staging ([32 features][256 samples] fp16 per n-tile), double buffered
 constexpr int SROW = 256 * 2 + 16;      // 16 B pad
 constexpr int STAGE = 32 * SROW;
@@ -111,11 +112,15 @@ struct Stager {
 MLI_FI void stage_tile(Stager& sg, uint8_t* lds, const f32x16& v, uint16_t* dst, int lane) {
   const int wave = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
   uint8_t* sb = lds + STAGE_OFF + sg.buf * STAGE + (4 * h) * SROW + (wave * 32 + c) * 2;
+#ifndef MLI_EXP_NOSTAGE
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const f16 x = (f16)v[i];
     *reinterpret_cast<uint16_t*>(sb + ((i & 3) + 8 * (i >> 2)) * SROW) = __builtin_bit_cast(uint16_t, x);
   }
+#else
+  if (v[0] == 1234.5f) *reinterpret_cast<uint16_t*>(sb) = 1;
+#endif
   sg.pend = dst;
   sg.pbuf = sg.buf;
   sg.buf ^= 1;
@@ -128,7 +133,9 @@ MLI_FI void stage_flush(Stager& sg, const uint8_t* lds, int S) {
   for (int u = 0; u < 2; ++u) {
     const int r = row + 16 * u;
     const u32x4 x = *reinterpret_cast<const u32x4*>(sb + r * SROW + col * 16);
-    *reinterpret_cast<u32x4*>(sg.pend + (size_t)r * S + col * 8) = x;
+    // streaming (non-temporal) store: the activations are re-read only by a later kernel, so
+    // they should not evict the weight chunks every phase re-reads from L2
+    __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(sg.pend + (size_t)r * S + col * 8));
   }
   sg.pend = nullptr;
 }
@@ -154,13 +161,17 @@ MLI_FI f32x16 chunk_mma(const uint8_t* chunk, const half8* X, int lane) {
 // Static store counts (for the counted vmcnt): STAGED = the layer stages its tiles (the
 // flush of tile t-1 at t >= 1 is 2 stores; the flush at t == 0 is decided at run time and
 // not counted), EPI = unconditional global stores per epilogue, MASKED = one mask store at
-// t == NT-1; pre(t) issues (and returns the count of) VMEM ops ahead of the weight DMAs.
+// t == NT-1; pre.issue(t) issues pre.count(t) VMEM ops ahead of the weight DMAs.
 template <int KS, int NT, bool STAGED, int EPI, bool MASKED, class Bytes, class Pre, class Epi>
 MLI_FI void run_layer(Ring& rg, uint8_t* lds, Stager& sg, int S, const half8* X, int lane, Bytes&& bytes,
                       Pre&& pre, Epi&& epi) {
+  // VMEM ops a phase issues after its weight DMAs (flush + epilogue stores), per t in the layer
+  auto stores = [](int t) MLI_LAMBDA_FI {
+    return ((t > 0 && STAGED) ? 2 : 0) + EPI + ((MASKED && t == NT - 1) ? 1 : 0);
+  };
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const int npre = pre(t);
+    pre.issue(t);
     ring_issue(rg, lds, bytes);
     if (t == 0) {
       if (sg.pend) stage_flush(sg, lds, S);
@@ -169,20 +180,25 @@ MLI_FI void run_layer(Ring& rg, uint8_t* lds, Stager& sg, int S, const half8* X,
     }
     const f32x16 acc = chunk_mma<KS>(lds + (rg.cur % NSLOT) * SLOT, X, lane);
     epi(t, acc);
-    // ops younger than chunk cur+1's DMAs (issued one phase earlier): this phase's mask DMAs,
-    // weight DMAs, flush and epilogue stores, plus the previous phase's flush and epilogue
-    const int f_now = (t > 0 && STAGED) ? 2 : 0;
-    const int f_prev = (t > 1 && STAGED) ? 2 : 0;
-    const int e_now = EPI + ((MASKED && t == NT - 1) ? 1 : 0);
-    const int e_prev = t > 0 ? EPI : 0;
-    vm_wait(npre + GLDS + f_now + e_now + f_prev + e_prev);
+    // retire chunk cur+1 (its DMAs went out DIST-1 phases ago): every VMEM op issued after
+    // them may stay in flight -- the weight DMAs of the DIST-1 later phases, the mask DMAs
+    // and stores of this and the previous phases (counted inside this layer, lower bound 0
+    // across the layer boundary)
+    int n = (DIST - 1) * GLDS + pre.count(t) + stores(t);
+#pragma unroll
+    for (int b = 1; b < DIST; ++b) {
+      if (t - b < 0) break;
+      n += stores(t - b) + (b < DIST - 1 ? pre.count(t - b) : 0);
+    }
+    vm_wait(n);
     block_sync();
     rg.cur++;
   }
 }
 
 struct NoPre {
-  MLI_FI int operator()(int) const { return 0; }
+  MLI_FI int count(int) const { return 0; }
+  MLI_FI void issue(int) const {}
 };
 
 // ---------------------------------------------------------------------- forward
@@ -248,10 +264,10 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
       }
     }
   }
-  // prologue: chunks 0 and 1 in flight, wait for chunk 0
-  ring_issue(rg, lds, bytes);
-  ring_issue(rg, lds, bytes);
-  vm_wait(GLDS);
+  // prologue: chunks 0 .. DIST-1 in flight, wait for chunk 0
+#pragma unroll
+  for (int d = 0; d < DIST; ++d) ring_issue(rg, lds, bytes);
+  vm_wait((DIST - 1) * GLDS);
   block_sync();
 
   Stager sg{nullptr, 0, 0};
@@ -350,9 +366,9 @@ __global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
   Ring rg;
   ring_start(rg, a.wbwd, BWD_CHUNKS, bytes);
   mask_dma(0);
-  ring_issue(rg, lds, bytes);
-  ring_issue(rg, lds, bytes);
-  vm_wait(GLDS);
+#pragma unroll
+  for (int d = 0; d < DIST; ++d) ring_issue(rg, lds, bytes);
+  vm_wait((DIST - 1) * GLDS);
   block_sync();
 
   half8 A[16], B[16];
@@ -376,14 +392,17 @@ __global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
           }
       }
     }
-    // the phase at t == 6 issues the next layer's mask DMA (before its weight DMAs)
-    auto pre = [&](int li) MLI_LAMBDA_FI {
-      return [&, li](int t) MLI_LAMBDA_FI {
-        if (t != 6) return 0;
-        mask_dma(hd * 4 + li + 1);
-        return 1;
-      };
+    // the phase whose weight DMAs fetch the next layer's first chunk (t == 8 - DIST) issues
+    // that layer's mask DMA just before them
+    struct MaskPre {
+      decltype(mask_dma)& dma;
+      int next_layer;
+      MLI_FI int count(int t) const { return t == 8 - DIST ? 1 : 0; }
+      MLI_FI void issue(int t) const {
+        if (t == 8 - DIST) dma(next_layer);
+      }
     };
+    auto pre = [&](int li) MLI_LAMBDA_FI { return MaskPre{mask_dma, hd * 4 + li + 1}; };
     auto mask_epi = [&](half8* out, int layer /* dZ index */, int li) MLI_LAMBDA_FI {
       return [&, out, layer, li](int t, const f32x16& acc) MLI_LAMBDA_FI {
         const u32x4 mv =

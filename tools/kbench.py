@@ -30,7 +30,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rays", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--membw", action="store_true", help="also time plain HBM write / copy streams")
     args = ap.parse_args()
+    if args.membw:
+        x = torch.empty(2 * 1024 ** 3, dtype=torch.float16, device="cuda")  # 4 GiB
+        y = torch.empty_like(x)
+        med, _ = timeit(lambda: x.fill_(1.0), 10)
+        print("fill 4 GiB            %.3f ms  %.2f TB/s write" % (med, 4 * 1024 ** 3 / med / 1e9))
+        med, _ = timeit(lambda: y.copy_(x), 10)
+        print("copy 4 GiB            %.3f ms  %.2f TB/s read+write" % (med, 8 * 1024 ** 3 / med / 1e9))
+        med, _ = timeit(lambda: x.sum(), 10)
+        print("sum 4 GiB             %.3f ms  %.2f TB/s read" % (med, 4 * 1024 ** 3 / med / 1e9))
+        del x, y
     from bench import kernel_flops
     from mli_nerf_amd import synthetic
     from mli_nerf_amd.configs import preset
