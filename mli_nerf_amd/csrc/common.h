@@ -94,4 +94,32 @@ MLI_FI float sel_mask(uint32_t mask, float hi, float lo) {
   return __builtin_bit_cast(float, r);
 }
 
+// ---------------------------------------------------------------- LDS-DMA pipelines
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_cvoid_t;
+
+// 16 B per lane global -> LDS (global_load_lds_dwordx4): lane l lands at lds_wave_base + 16 l
+MLI_FI void glds16(const void* g, uint8_t* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_cvoid_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+// s_waitcnt vmcnt(n) for a count known after unrolling (the switch folds)
+MLI_FI void vm_wait(int n) {
+  switch (n) {
+#define MLI_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    MLI_VMW(1) MLI_VMW(2) MLI_VMW(3) MLI_VMW(4) MLI_VMW(5) MLI_VMW(6) MLI_VMW(7) MLI_VMW(8)
+    MLI_VMW(9) MLI_VMW(10) MLI_VMW(11) MLI_VMW(12) MLI_VMW(13) MLI_VMW(14) MLI_VMW(15) MLI_VMW(16)
+#undef MLI_VMW
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// LDS writes visible to the workgroup; no vector-memory drain (raw barrier: __syncthreads'
+// fence would wait for every outstanding DMA and store)
+MLI_FI void block_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 #define MLI_LAUNCH_CHECK() return (int)hipGetLastError()

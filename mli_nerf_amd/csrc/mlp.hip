@@ -24,9 +24,6 @@
 
 namespace {
 
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) const void gbl_cvoid_t;
-
 constexpr int THREADS = 512;
 constexpr int WAVES = 8;
 constexpr int CH(int ks) { return ks * 1024 + 128; }
@@ -43,28 +40,6 @@ constexpr int STAGE_OFF = NSLOT * SLOT;
 constexpr int MASK_OFF = STAGE_OFF + 2 * STAGE;  // backward: 2 x 8 KiB ReLU-mask blocks
 constexpr int LDS_FWD = STAGE_OFF + 2 * STAGE;
 constexpr int LDS_BWD = MASK_OFF + 2 * 8192;
-
-MLI_FI void glds16(const void* g, uint8_t* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((gbl_cvoid_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
-}
-
-// s_waitcnt vmcnt(n) for a count known after unrolling (the switch folds)
-MLI_FI void vm_wait(int n) {
-  switch (n) {
-#define MLI_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-    MLI_VMW(1) MLI_VMW(2) MLI_VMW(3) MLI_VMW(4) MLI_VMW(5) MLI_VMW(6) MLI_VMW(7) MLI_VMW(8)
-    MLI_VMW(9) MLI_VMW(10) MLI_VMW(11) MLI_VMW(12)
-#undef MLI_VMW
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-
-// LDS writes visible to the workgroup; no vector-memory drain (raw barrier).
-MLI_FI void block_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
 
 // ---------------------------------------------------------------------- weight ring
 struct Ring {
