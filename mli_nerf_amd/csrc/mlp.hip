@@ -289,7 +289,7 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
           if (t == 7) {
             u32x4* mp = reinterpret_cast<u32x4*>(a.masks) +
                         ((size_t)(hd * 4 + layer) * (S / 32) + tile) * 64 + lane;
-            *mp = u32x4{mbits[0], mbits[1], mbits[2], mbits[3]};
+            __builtin_nontemporal_store(u32x4{mbits[0], mbits[1], mbits[2], mbits[3]}, mp);
           }
         }
       };

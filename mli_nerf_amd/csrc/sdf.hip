@@ -90,10 +90,10 @@ MLI_FI float sdf_from_enc(const uint8_t* lds, const half8 (&enc)[8], int lane, f
       sp[i] = softplus100(acc[i]);
       part = fmaf(ws[i], sp[i], part);
     }
-    if (h0_tile) {
+    if (h0_tile) {  // read by the next kernel only: non-temporal
       half8* dst = reinterpret_cast<half8*>(h0_tile) + (2 * t) * 64 + lane;
-      dst[0] = acc_to_frag(sp, 0);
-      dst[64] = acc_to_frag(sp, 1);
+      __builtin_nontemporal_store(acc_to_frag(sp, 0), dst);
+      __builtin_nontemporal_store(acc_to_frag(sp, 1), dst + 64);
     }
   }
   part += __shfl_xor(part, 32);

@@ -36,7 +36,8 @@ MLI_FI void stage_load(u32x4 (&st)[LOADS], const uint16_t* __restrict__ base, in
   for (int u = 0; u < LOADS; ++u) {
     const int id = u * 512 + tid, row = min(id >> 3, ROWS - 1), col = id & 7;
     const int gr = min(t * ROWS + row, n_rows - 1);
-    st[u] = *reinterpret_cast<const u32x4*>(base + gr * S + k + col * 8);
+    // streamed once: non-temporal (leave L2 to the dW atomics)
+    st[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base + gr * S + k + col * 8));
   }
 }
 
