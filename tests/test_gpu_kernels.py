@@ -48,3 +48,29 @@ def test_wgrad_matches_torch(S):
         err_b = ((db - rb).abs().max() / rb.abs().max()).item()
         print("job %d %s: rel err dW %.2e db %.2e" % (i, tuple(rw.shape), err_w, err_b))
         assert err_w < 1e-4 and err_b < 1e-4, (i, err_w, err_b)
+
+
+@pytest.mark.parametrize("S", [65536, 8384])
+def test_wgrad_wide_jobs_sharing_b(S):
+    """The layer-0 weight gradients of the three heads as the engine issues them: three WIDE
+    jobs (M = 256, K = 304) streaming the SAME feature-major input x0T (ragged S too)."""
+    _need_gpu()
+    from mli_nerf_amd import _lib as L
+    g = torch.Generator(device="cpu").manual_seed(5)
+    b = (torch.randn(304, S, generator=g) * 0.5).half().to(DEV)
+    jobs, refs, keep = [], [], [b]
+    for _ in range(3):
+        a = (torch.randn(256, S, generator=g) * 0.5).half().to(DEV)
+        dw = torch.zeros(256, 304, device=DEV)
+        db = torch.zeros(256, device=DEV)
+        keep += [a, dw, db]
+        jobs.append(L.WgradJob(L.ptr(a), L.ptr(b), 256, 304, L.ptr(dw), L.ptr(db), 304))
+        refs.append((a.float() @ b.float().t(), a.float().sum(1), dw, db))
+    arr = (L.WgradJob * 3)(*jobs)
+    L.call("mli_wgrad", L.WgradArgs(S, 3, C.cast(arr, C.c_void_p), 2))
+    torch.cuda.synchronize()
+    for i, (rw, rb, dw, db) in enumerate(refs):
+        err_w = ((dw - rw).abs().max() / rw.abs().max()).item()
+        err_b = ((db - rb).abs().max() / rb.abs().max()).item()
+        print("wide job %d: rel err dW %.2e db %.2e" % (i, err_w, err_b))
+        assert err_w < 1e-4 and err_b < 1e-4
