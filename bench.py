@@ -170,7 +170,7 @@ def run_infer(args, world, rank, dev):
         threads = min(16, os.cpu_count() or 1)
         torch.set_num_threads(threads)
         sd = synthetic.make_state_dict(log2T=22, seed=0)
-        pcfg = o_render.PathCfg(n_fine=args.fine)
+        pcfg = oracle_cfg(cfg)
         data = {k: v.cpu() for k, v in frames[-1].items()}  # the last rendered frame is `out`
         n_cpu = args.cpu_rays * 4
         data["ray_idx"] = torch.arange(n_cpu)[None] * (n_pix // n_cpu)
@@ -195,7 +195,17 @@ def run_infer(args, world, rank, dev):
         dist.destroy_process_group()
 
 
-def cpu_baseline(R_cpu, steps, threads):
+def oracle_cfg(cfg):
+    """The oracle's PathCfg for a preset (same sampling, background, bounds as the GPU run)."""
+    from oracle import render as o_render
+    r = cfg.model.render
+    return o_render.PathCfg(n_coarse=r.num_samples.coarse, n_fine=r.num_samples.fine,
+                            n_hier=r.num_sample_hierarchy, white_bg=bool(cfg.model.background.white),
+                            bounding="box" if cfg.data.get("bounding_type") == "box" else "sphere",
+                            aabb=tuple(cfg.data.get("bounding_box_aabb", (-1, -1, -1, 1, 1, 1))))
+
+
+def cpu_baseline(cfg, R_cpu, steps, threads):
     """The CPU oracle (fp32 PyTorch restatement of the reference path) timed on the host:
     stage-b forward + losses + backward on R_cpu rays of the same workload."""
     from mli_nerf_amd import synthetic
@@ -203,14 +213,15 @@ def cpu_baseline(R_cpu, steps, threads):
     torch.set_num_threads(threads)
     sd = synthetic.make_state_dict(log2T=22)
     sd = {k: v.requires_grad_(k.startswith("neural_rgb")) for k, v in sd.items()}
-    pcfg = o_render.PathCfg()
-    data = synthetic.make_batch(R_cpu, frame=0, seed=7)
+    pcfg = oracle_cfg(cfg)
+    Hh, W = cfg.data.train.image_size
+    data = synthetic.make_batch(R_cpu, H=Hh, W=W, frame=0, seed=7)
     u = synthetic.stratified_uniforms(R_cpu, pcfg.n_coarse, seed=7)
     times = []
     out = psnr = None
     for i in range(steps + 2):  # 2 untimed warm-up steps
         t0 = time.perf_counter()
-        out = o_render.forward(sd, pcfg, data, u=u, training=True, progress=0.0)
+        out = o_render.forward(sd, pcfg, data, u=u, training=True, progress=0.0, width=W, height=Hh)
         total, _, psnr = o_render.stage_b_losses(out, data, pcfg)
         total.backward()
         for v in sd.values():
@@ -316,7 +327,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = min(16, os.cpu_count() or 1)
-        cb, data_cpu, u_cpu, psnr_cpu = cpu_baseline(args.cpu_rays, args.cpu_steps, threads)
+        cb, data_cpu, u_cpu, psnr_cpu = cpu_baseline(cfg, args.cpu_rays, args.cpu_steps, threads)
         result["cpu_baseline"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in cb.items()}
         result["speedup_vs_cpu"] = round(value / cb["value"], 1)
         # PSNR agreement on the CPU sample's rays (same weights, rays, uniforms)
