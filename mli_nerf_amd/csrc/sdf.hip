@@ -34,6 +34,23 @@ struct SdfKArgs {
   mli_sdf_args a;
 };
 
+// The packed SDF block (70 KiB) -> LDS by LDS-DMA: every 16 B piece issued back to back,
+// one wait (a load -> store loop would pay one global round trip per 4 KiB).  The DMA lands
+// lane-linearly in whole 1 KiB wave pieces, so the kernels allocate LDS_SDF (rounded up):
+// the tail lanes repeat the last piece into the padding.
+constexpr int PIECES = MLI_SDF_PACK_BYTES / 16;  // 4481 (the last one: b_sdf)
+constexpr int LDS_SDF = ((PIECES + 63) / 64) * 64 * 16;
+MLI_FI void load_weights(uint8_t* lds, const void* wsdf) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(wsdf);
+  for (int base = wave * 64; base < PIECES; base += nw * 64) {
+    const int piece = min(base + lane, PIECES - 1);  // the tail lanes repeat the last piece
+    glds16(src + piece * 16, lds + base * 16);
+  }
+  vm_wait(0);
+  __syncthreads();
+}
+
 // Row constants of n-tile t for this lane half: 16 floats of array `arr`.
 MLI_FI void load_rowc(const uint8_t* lds, int arr, int t, int h, float (&v)[16]) {
   const f32x4* p = reinterpret_cast<const f32x4*>(lds + ROWC_OFF + arr * ROWC_ARRAY + (t * 2 + h) * 64);
@@ -252,12 +269,7 @@ constexpr int MLP_WAVES = 8;  // 8 waves share the 70 KiB LDS weight block: 2 bl
 
 __global__ __launch_bounds__(MLP_WAVES * 64) void field_mlp_kernel(mli_sdf_args a, int tile0, int tile1) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  {
-    const u32x4* src = reinterpret_cast<const u32x4*>(a.wsdf);
-    u32x4* dst = reinterpret_cast<u32x4*>(lds);
-    for (int o = threadIdx.x; o < MLI_SDF_PACK_BYTES / 16; o += blockDim.x) dst[o] = src[o];
-  }
-  __syncthreads();
+  load_weights(lds, a.wsdf);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int n_total = a.R * a.n_per_ray;
@@ -318,12 +330,7 @@ __global__ __launch_bounds__(MLP_WAVES * 64) void field_mlp_kernel(mli_sdf_args 
 // SDF only (sampling rounds): one point per lane, encode + layer 0 + sdf head fused.
 __global__ __launch_bounds__(256) void sdf_kernel(mli_sdf_args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  {
-    const u32x4* src = reinterpret_cast<const u32x4*>(a.wsdf);
-    u32x4* dst = reinterpret_cast<u32x4*>(lds);
-    for (int o = threadIdx.x; o < MLI_SDF_PACK_BYTES / 16; o += blockDim.x) dst[o] = src[o];
-  }
-  __syncthreads();
+  load_weights(lds, a.wsdf);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int n_total = a.R * a.n_per_ray;
@@ -409,7 +416,7 @@ extern "C" int mli_sdf(const mli_sdf_args* a, mli_stream_t s) {
   if (a->mode == MLI_SDF_MODE_SDF) {
     int blocks = (tiles + SDF_WAVES - 1) / SDF_WAVES;
     if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(sdf_kernel, dim3(blocks), dim3(256), MLI_SDF_PACK_BYTES, (hipStream_t)s, *a);
+    hipLaunchKernelGGL(sdf_kernel, dim3(blocks), dim3(256), LDS_SDF, (hipStream_t)s, *a);
     MLI_LAUNCH_CHECK();
   }
   if (a->enc == nullptr || a->h0 == nullptr || a->grad == nullptr) return (int)hipErrorInvalidValue;
@@ -422,7 +429,7 @@ extern "C" int mli_sdf(const mli_sdf_args* a, mli_stream_t s) {
     hipLaunchKernelGGL(encode5_kernel, dim3((t1 - t0 + 3) / 4), dim3(256), 0, (hipStream_t)s, *a, t0, t1);
     int blocks = (t1 - t0 + MLP_WAVES - 1) / MLP_WAVES;
     if (blocks > 512) blocks = 512;
-    hipLaunchKernelGGL(field_mlp_kernel, dim3(blocks), dim3(MLP_WAVES * 64), MLI_SDF_PACK_BYTES, (hipStream_t)s,
+    hipLaunchKernelGGL(field_mlp_kernel, dim3(blocks), dim3(MLP_WAVES * 64), LDS_SDF, (hipStream_t)s,
                        *a, t0, t1);
     const int e = (int)hipGetLastError();
     if (e) return e;
