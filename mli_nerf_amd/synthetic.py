@@ -43,8 +43,11 @@ def _weight_norm_pair(w):
     return w.norm(dim=1, keepdim=True), w.clone()
 
 
-def make_state_dict(log2T=GRID_DEFAULTS["log2T"], seed=0, s_var=3.0, enc_std=1e-2, table_amp=0.1):
-    """Reference state-dict keys (no DDP ``module.`` prefix) -> fp32 CPU tensors."""
+def make_state_dict(log2T=GRID_DEFAULTS["log2T"], seed=0, s_var=3.0, enc_std=1e-2, table_amp=0.1,
+                    heads="rgb_r_s"):
+    """Reference state-dict keys (no DDP ``module.`` prefix) -> fp32 CPU tensors.
+    ``heads``: LumenRGB network_mode -- 'rgb_r_s' (stage b, three heads) or 'rgb' (stage a,
+    the single 294 -> 3 head, drawn first from the same stream, so it equals stage b's mlp)."""
     sd = {}
     table, total = level_table(log2T=log2T)
     g = _gen(seed * 100 + 5)
@@ -63,7 +66,7 @@ def make_state_dict(log2T=GRID_DEFAULTS["log2T"], seed=0, s_var=3.0, enc_std=1e-
                                               + math.sqrt(math.pi / HIDDEN))
     sd["neural_sdf.mlp.linear_sdf.bias"] = torch.full((1,), -0.5)
     g = _gen(seed * 100 + 6)
-    for name, k_in, k_out in HEAD_SPECS:
+    for name, k_in, k_out in (HEAD_SPECS[:1] if heads == "rgb" else HEAD_SPECS):
         dims = [k_in] + [HIDDEN] * 4 + [k_out]
         for li in range(5):
             fan_in, fan_out = dims[li], dims[li + 1]

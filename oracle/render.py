@@ -45,6 +45,9 @@ class PathCfg:
         render=1.0, eikonal=0.1, curvature=5e-4, intrinsic=1.0, regularize_re=1.0))
     intrinsic_ranges: tuple = ((0.0, 1.0), (0.0, 1.0))   # syn_hotdog_b.yaml:10-16
     re_factors: tuple = (10.0, 1.0, 1.0)                   # syn_hotdog_b.yaml:19-22
+    rgb_mode: str = "rgb_r_s"       # LumenRGB network_mode; "rgb" = stage a (modules.py:50-55)
+    active_levels: int = None       # coarse-to-fine mask (modules.py:91-113); None = all levels
+    anneal_levels: int = None       # tap epsilon level (modules.py:102-107); None = all levels
 
     @property
     def n_samples(self):
@@ -55,10 +58,12 @@ class PathCfg:
         return np.exp((np.log(r_max) - np.log(r_min)) / (self.levels - 1))
 
     def normal_eps(self):
-        # neuralangelo/utils/modules.py:51-54 (resolutions) + :102-107 (c2f disabled in stage b)
+        # neuralangelo/utils/modules.py:51-54 (resolutions) + :102-107 (c2f: resolution of
+        # level anneal_levels - 1; disabled in stage b -> the finest level)
         g = self.growth_rate()
         res = [np.floor(2 ** self.min_logres * g ** lv).astype(int) + 1 for lv in range(self.levels)]
-        return 1.0 / res[-1]
+        lv = self.levels if self.anneal_levels is None else self.anneal_levels
+        return 1.0 / res[lv - 1]
 
     def table(self):
         return hashgrid.level_table(self.levels, self.log2T, 2 ** self.min_logres, self.growth_rate())
@@ -150,6 +155,11 @@ def sdf_net(weights, cfg, pts, with_feat):
     x01 = (flat - lo) / (hi - lo)
     table, _ = cfg.table()
     enc = hashgrid.encode(x01, weights["neural_sdf.tcnn_encoding.params"], table)
+    if cfg.active_levels is not None:
+        # coarse-to-fine mask (modules.py:91-93,110-113): levels >= active_levels -> 0
+        mask = torch.zeros_like(enc)
+        mask[..., :cfg.active_levels * 8] = 1
+        enc = enc * mask
     inp = torch.cat([flat, enc], dim=-1)
     h0 = softplus100(F.linear(inp, wn(weights, "neural_sdf.mlp.linears.0"),
                               weights["neural_sdf.mlp.linears.0.bias"]))
@@ -271,12 +281,15 @@ def head_mlp(weights, name, x):
     return h
 
 
-def rgb_heads(weights, pts, normals, rays_unit, feats, pts_light):
-    """LumenRGB.forward, network_mode 'rgb_r_s' (NeuralLumen/utils/modules.py:106-163).
+def rgb_heads(weights, pts, normals, rays_unit, feats, pts_light, mode="rgb_r_s"):
+    """LumenRGB.forward, network_mode 'rgb_r_s' (NeuralLumen/utils/modules.py:106-163), or
+    the single-head mode 'rgb' of stage a (:164-174, same input order as 'mlp').
     Quirk kept: SH of the raw (un-normalised) light position (:109)."""
     view = sh16(rays_unit)
     light = sh16(pts_light)
     x_rgb = torch.cat([pts, view, normals, feats, light], dim=-1)
+    if mode == "rgb":
+        return head_mlp(weights, "mlp", x_rgb).sigmoid(), None, None
     x_r = torch.cat([pts, normals, feats], dim=-1)
     x_s = torch.cat([pts, normals, feats, light], dim=-1)
     return (head_mlp(weights, "mlp", x_rgb).sigmoid(),
@@ -320,16 +333,22 @@ def render_rays(weights, cfg, center, ray_unit, pts_light, u=None, training=True
     normals = F.normalize(grads, dim=-1)
     rays_n = ray_unit[..., None, :].expand_as(pts)
     light_n = pts_light[..., None, :].expand_as(pts)
-    rgbs, o_r, o_s = rgb_heads(weights, pts, normals, rays_n, feats, light_n)
+    rgbs, o_r, o_s = rgb_heads(weights, pts, normals, rays_n, feats, light_n, cfg.rgb_mode)
     alphas = neus_alphas(weights["s_var"], ray_unit, sdfs, grads, dists, far, progress, cfg.anneal_end)
     w = exclusive_transmittance_weights(alphas)
     rgb = (rgbs * w).sum(2)
-    acc_r = (o_r * w).sum(2)
-    acc_s = (o_s * w).sum(2)
     opacity = w.sum(2)
-    if cfg.white_bg:
-        rgb, acc_r, acc_s = rgb + (1 - opacity), acc_r + (1 - opacity), acc_s + (1 - opacity)
-    out = dict(rgb=rgb, o_r=acc_r, o_s=acc_s, o_re=rgb - acc_r * acc_s,
+    if cfg.rgb_mode == "rgb":  # NeuralLumen/model.py:300-303
+        acc_r = acc_s = o_re = None
+        if cfg.white_bg:
+            rgb = rgb + (1 - opacity)
+    else:
+        acc_r = (o_r * w).sum(2)
+        acc_s = (o_s * w).sum(2)
+        if cfg.white_bg:
+            rgb, acc_r, acc_s = rgb + (1 - opacity), acc_r + (1 - opacity), acc_s + (1 - opacity)
+        o_re = rgb - acc_r * acc_s
+    out = dict(rgb=rgb, o_r=acc_r, o_s=acc_s, o_re=o_re,
                outside=outside, dists=dists, weights=w, gradients=grads, hessians=hess,
                sdfs=sdfs, alphas=alphas, rgbs=rgbs, rgbs_r=o_r, rgbs_s=o_s,
                opacity=None, gradient=None)
@@ -386,6 +405,32 @@ def stage_b_losses(out, data, cfg):
     total = sum(losses[k] * cfg.loss_w[k] for k in cfg.loss_w)
     psnr = -10 * torch.log10(F.mse_loss(out["rgb"], data["image_sampled"]))
     return total, losses, psnr
+
+
+def stage_a_losses(out, data, curvature_weight, eikonal_weight=0.1, render_weight=1.0):
+    """Stage-a loss (NeuralLumen/trainer.py:133-141 without the intrinsic terms; weights
+    base.yaml:28-31, the curvature weight scheduled by neuralangelo/trainer.py:56-63)."""
+    mask = (~out["outside"]).float()
+    g_err = ((out["gradients"].norm(dim=-1) - 1.0) ** 2).nan_to_num(nan=0.0, posinf=0.0, neginf=0.0)
+    lap = out["hessians"].sum(-1).abs().nan_to_num(nan=0.0, posinf=0.0, neginf=0.0)
+    losses = dict(render=F.l1_loss(out["rgb"], data["image_sampled"]) * 3,
+                  eikonal=(g_err * mask).mean(), curvature=(lap * mask).mean())
+    w = dict(render=render_weight, eikonal=eikonal_weight, curvature=curvature_weight)
+    total = sum(losses[k] * w[k] for k in losses)
+    psnr = -10 * torch.log10(F.mse_loss(out["rgb"], data["image_sampled"]))
+    return total, losses, psnr
+
+
+def stage_a_param_names(levels=16):
+    """Every parameter is trained in stage a (no partial_grad; get_param_groups returns
+    self.parameters(), NeuralLumen/model.py:422-438)."""
+    names = ["neural_sdf.tcnn_encoding.params"]
+    for li in range(2):
+        names += ["neural_sdf.mlp.linears.%d.%s" % (li, p) for p in ("weight_g", "weight_v", "bias")]
+    names += ["neural_sdf.mlp.linear_sdf.weight", "neural_sdf.mlp.linear_sdf.bias"]
+    for li in range(5):
+        names += ["neural_rgb.mlp.linears.%d.%s" % (li, p) for p in ("weight_g", "weight_v", "bias")]
+    return names + ["s_var"]
 
 
 def head_param_names():

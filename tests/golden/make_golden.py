@@ -41,6 +41,15 @@ CASES = {
     "savannah_r64_n32_box": ("rene_savannah_b", 64, 16, 4, 4, 14, 3.0, 0.0, True, {}),
 }
 
+# Stage a (syn_hotdog_a.yaml: LumenRGB mode 'rgb', coarse-to-fine hash grid, every parameter
+# trained incl. the hash table and s_var): name -> (config, R, Nc, Nf, H, log2T, s_var, iteration)
+STAGE_A_CASES = {
+    "hotdog_a_r64_n32_it20k": ("syn_hotdog_a", 64, 16, 4, 4, 14, 3.0, 20000),
+    "hotdog_a_r32_n128_it80k": ("syn_hotdog_a", 32, 64, 16, 4, 14, 4.0, 80000),
+}
+MAX_ITER = 500000      # neuralangelo/configs/base.yaml:13
+WARM_UP_END = 5000     # base.yaml optim.sched.warm_up_end
+
 
 def install_stubs():
     sys.modules["cv2"] = types.ModuleType("cv2")
@@ -207,9 +216,83 @@ def check(name, fix, o_out, o_losses, o_total, o_grads):
             if ref is None:
                 ref = fix["grad." + k + ":strided"]
                 g = g.flatten()[::97]
+            if ref.dim() == 0:
+                ref, g = ref.reshape(1), g.reshape(1)
             err = (ref - g).abs().max().item()
             assert err <= 1e-5 + 1e-3 * ref.abs().max().item(), (name, k, err)
     print("%s: oracle matches reference (worst err/tol %.3f)" % (name, worst))
+
+
+def curvature_weight(it, init, growth_rate, anneal_levels):
+    """neuralangelo/trainer.py:56-63 get_curvature_weight."""
+    if it <= WARM_UP_END:
+        return it / WARM_UP_END * init
+    return init / growth_rate ** (anneal_levels - 1)
+
+
+def run_stage_a_case(name, spec):
+    """Stage-a train step of the reference model: forward, the stage-a losses with the
+    reference's own loss functions, backward into EVERY parameter (hash table included)."""
+    from projects.nerf.utils import nerf_util
+    from projects.NeuralLumen.model import Model
+    from projects.neuralangelo.utils.misc import eikonal_loss, curvature_loss
+    config, R, Nc, Nf, H, log2T, s_var, it = spec
+    nerf_util.sample_dists.__defaults__ = ("cpu",)
+    cfg = reference_cfg(config, R, Nc, Nf, H, log2T)
+    H_img, W_img = cfg.data.train.image_size
+    model = Model(cfg.model, cfg.data)
+    assert model.neural_rgb.network_mode == "rgb"
+    sd = synthetic.make_state_dict(log2T=log2T, seed=0, s_var=s_var, heads="rgb")
+    load_weights(model, sd)
+    table = model.neural_sdf.tcnn_encoding.params.detach().clone().requires_grad_(True)
+    model.neural_sdf.tcnn_encoding.params = table
+    # neuralangelo/trainer.py:28-34,65-76 (_start_of_iteration)
+    model.neural_sdf.warm_up_end = WARM_UP_END
+    model.progress = progress = it / MAX_ITER
+    model.neural_sdf.set_active_levels(it)
+    model.neural_sdf.set_normal_epsilon()
+    w_curv = float(curvature_weight(it, float(cfg.trainer.loss_weight.curvature),
+                                    float(model.neural_sdf.growth_rate), int(model.neural_sdf.anneal_levels)))
+    data = synthetic.make_batch(R, H=H_img, W=W_img, frame=3)
+    torch.manual_seed(1234)
+    u = torch.rand(1, R, Nc)
+    model.train()
+    torch.manual_seed(1234)
+    out = model(data)
+    w = cfg.trainer.loss_weight
+    losses = dict(render=torch.nn.L1Loss()(out["rgb"], data["image_sampled"]) * 3,
+                  eikonal=eikonal_loss(out["gradients"], outside=out["outside"]),
+                  curvature=curvature_loss(out["hessians"], outside=out["outside"]))
+    total = losses["render"] * w.render + losses["eikonal"] * w.eikonal + losses["curvature"] * w_curv
+    total.backward()
+    grads = {k: p.grad for k, p in model.named_parameters() if p.grad is not None}
+    grads["neural_sdf.tcnn_encoding.params"] = table.grad
+    fix = dict(R=R, Nc=Nc, Nf=Nf, H=H, log2T=log2T, s_var=s_var, progress=progress, train=True,
+               config=config, H_img=H_img, W_img=W_img, iteration=it, u=u,
+               active_levels=int(model.neural_sdf.active_levels), anneal_levels=int(model.neural_sdf.anneal_levels),
+               normal_eps=float(model.neural_sdf.normal_eps), curvature_weight=w_curv)
+    for k in ("rgb", "dists", "weights", "gradients", "hessians", "outside"):
+        fix["out." + k] = out[k].detach().clone()
+    fix["loss.total"] = total.detach()
+    for k, v in losses.items():
+        fix["loss." + k] = v.detach()
+    dig = grad_digest({k: v for k, v in grads.items() if k != "neural_sdf.tcnn_encoding.params"})
+    tg = table.grad.flatten()
+    dig["neural_sdf.tcnn_encoding.params:strided"] = tg[::97].clone()
+    dig["neural_sdf.tcnn_encoding.params:sum"] = tg.double().sum().float()
+    dig["neural_sdf.tcnn_encoding.params:abssum"] = tg.double().abs().sum().float()
+    fix.update({"grad." + k: v for k, v in dig.items()})
+    # oracle check
+    pcfg = path_cfg(cfg, Nc, Nf, H, log2T)
+    pcfg.rgb_mode, pcfg.active_levels, pcfg.anneal_levels = "rgb", fix["active_levels"], fix["anneal_levels"]
+    sd_o = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    o_out = o_render.forward(sd_o, pcfg, data, u=u, training=True, progress=progress, width=W_img, height=H_img)
+    o_total, o_losses, _ = o_render.stage_a_losses(o_out, data, w_curv)
+    o_total.backward()
+    check(name, fix, o_out, o_losses, o_total, {k: sd_o[k].grad for k in grads})
+    path = os.path.join(HERE, name + ".pt")
+    torch.save(fix, path)
+    print("wrote %s (%.1f KB)" % (path, os.path.getsize(path) / 1024))
 
 
 def main():
@@ -219,6 +302,10 @@ def main():
         if only and name not in only:
             continue
         run_case(name, spec)
+    for name, spec in STAGE_A_CASES.items():
+        if only and name not in only:
+            continue
+        run_stage_a_case(name, spec)
 
 
 if __name__ == "__main__":

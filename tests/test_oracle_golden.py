@@ -63,3 +63,41 @@ def test_level_table_matches_product_side():
     from oracle.hashgrid import level_table as oracle_table
     assert product_table()[0] == oracle_table()[0]
     assert product_table()[1] == 45724048  # fp32 tcnn scale arithmetic: level 5 res = 129
+
+
+STAGE_A_CASES = ["hotdog_a_r64_n32_it20k", "hotdog_a_r32_n128_it80k"]
+
+
+@pytest.mark.parametrize("name", STAGE_A_CASES)
+def test_oracle_stage_a_matches_reference_golden(golden, name):
+    """Stage a (syn_hotdog_a): single 'rgb' head, coarse-to-fine mask, tap epsilon of the
+    annealed level, gradients of EVERY parameter incl. the hash table and s_var."""
+    fx = golden(name)
+    cfg = case_cfg({**fx, "config": "syn_hotdog_b"})
+    cfg.rgb_mode, cfg.active_levels, cfg.anneal_levels = "rgb", fx["active_levels"], fx["anneal_levels"]
+    assert abs(cfg.normal_eps() - fx["normal_eps"]) < 1e-12
+    sd = synthetic.make_state_dict(log2T=fx["log2T"], seed=0, s_var=fx["s_var"], heads="rgb")
+    sd = {k: v.requires_grad_(True) for k, v in sd.items()}
+    out = o_render.forward(sd, cfg, data := synthetic.make_batch(fx["R"], H=fx["H_img"], W=fx["W_img"], frame=3),
+                           u=fx["u"], training=True, progress=fx["progress"], width=fx["W_img"], height=fx["H_img"])
+    for key, ref in fx.items():
+        if not key.startswith("out."):
+            continue
+        got = out[key[4:]].detach()
+        if ref.dtype == torch.bool:
+            assert torch.equal(got, ref), key
+        else:
+            torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5, msg=key)
+    total, losses, _ = o_render.stage_a_losses(out, data, fx["curvature_weight"])
+    for k, v in losses.items():
+        torch.testing.assert_close(v.detach(), fx["loss." + k], rtol=1e-5, atol=1e-6)
+    total.backward()
+    for name_p in o_render.stage_a_param_names():
+        g = sd[name_p].grad
+        if "grad." + name_p in fx:
+            torch.testing.assert_close(g.reshape(fx["grad." + name_p].shape), fx["grad." + name_p],
+                                       rtol=1e-4, atol=1e-7)
+        else:
+            torch.testing.assert_close(g.flatten()[::97], fx["grad." + name_p + ":strided"], rtol=1e-4, atol=1e-7)
+            torch.testing.assert_close(g.double().sum().float(), fx["grad." + name_p + ":sum"],
+                                       rtol=1e-4, atol=1e-6)
