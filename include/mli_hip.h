@@ -35,7 +35,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mli_stream_t; /* == hipStream_t */
 
-#define MLI_ABI_VERSION 5
+#define MLI_ABI_VERSION 6
 #define MLI_HIDDEN 256
 #define MLI_LEVELS 16
 #define MLI_LEVEL_FEAT 8
@@ -119,6 +119,8 @@ typedef struct {
   uint16_t* h0;           /* frag image [S/32][16][64][8] (FIELD) */
   uint16_t* enc;          /* FIELD scratch: hash encodings of the 5 points (center + 4 taps)
                              as MFMA B-fragment images [S/32][5][8][64][8] fp16 (S*640 halves) */
+  int active_levels;      /* coarse-to-fine mask (modules.py:91-93,110-113): levels >= this
+                             encode to 0 (stage b / c2f off: MLI_LEVELS)                     */
 } mli_sdf_args;
 int mli_sdf(const mli_sdf_args* a, mli_stream_t s);
 
@@ -165,6 +167,7 @@ typedef struct {
   uint16_t* x0T;          /* [MLI_HEAD_K0][S] feature-major head input                      */
   uint16_t* xT;           /* [3 heads][4 layers][256][S] feature-major X1..X4               */
   uint32_t* masks;        /* [3][4][S/32][64][4] ReLU bit masks of X1..X4                   */
+  int n_heads;            /* 3: LumenRGB 'rgb_r_s' (stage b); 1: mode 'rgb' (stage a, head mlp) */
 } mli_rgb_fwd_args;
 int mli_rgb_fwd(const mli_rgb_fwd_args* a, mli_stream_t s);
 
@@ -236,6 +239,118 @@ typedef struct {
 } mli_wgrad_args;
 int mli_wgrad(const mli_wgrad_args* a, mli_stream_t s);
 
+/* ---------------------------------------------------------------- stage a (geometry training)
+ * Backward of the whole render w.r.t. the geometry: replaces autograd through
+ * compute_neus_alphas (neuralangelo/model.py:492-515), alpha_compositing_weights/composite
+ * (render.py:87-112), the single 'rgb' head (NeuralLumen/utils/modules.py:164-174) down to
+ * its inputs (feat, normals), F.normalize, compute_gradients taps=4 (modules.py:157-175),
+ * MLPforNeuralSDF (mlp.py:55-69), the coarse-to-fine mask and the tcnn HashGrid backward
+ * (scatter-add into the table; restated in oracle/hashgrid.py).  grad_scale: the power-of-two
+ * loss scale of every fp16 gradient image (undone in fp32 at the outputs). */
+
+/* Composite backward with geometry terms, one wave per ray: dz4 (rgb head output grads,
+ * scaled), d total / d sdf (after the outside overwrite), d total / d grad through the NeuS
+ * iter_cos, and d total / d s_var (written by a second launch). */
+typedef struct {
+  int R, N;
+  const float* dists; const float* far_; const float* ray_unit;
+  const float* sdf; const float* grad; const float* y;   /* y: [N][R][8], rgb in 0..2 */
+  const float* s_var;
+  float anneal;
+  int white_bg;
+  const float* d_rgb;     /* [R,3] d total / d rgb */
+  float grad_scale;
+  float* dz4;             /* [N][R][8] scaled */
+  float* d_sdf;           /* [N][R] */
+  float* d_grad;          /* [N][R][3] */
+  float* d_inv_s_acc;     /* device scalar, zeroed by the caller */
+  float* d_s_var;         /* device scalar out: exp(s_var) * d_inv_s */
+} mli_composite_bwd_geo_args;
+int mli_composite_bwd_geo(const mli_composite_bwd_geo_args* a, mli_stream_t s);
+
+/* dX chain of the single head down to its inputs, then through SDF layer 1:
+ * dZ3..dZ0 (feature-major, for the head dW), dX0 -> d feat (frag order) and d normal,
+ * dZ1sdf = d feat * softplus'(z1) (feature-major, for dW of neural_sdf.mlp.linears.1) and
+ * d h0 of the center point = W1^T dZ1sdf (frag image, ACC order as the h0 image). */
+typedef struct {
+  int R, N;
+  const float* dz4;       /* [N][R][8] */
+  const void* wgeo;       /* packed chunks (mli_pack): W4^T, W3^T, W2^T, W1^T, W0^T (9 n-tiles),
+                             W1sdf^T of the stage-a layout (mli_nerf_amd/layout.py geo_plan) */
+  const uint32_t* masks;  /* head 0 masks from mli_rgb_fwd */
+  const uint16_t* feat_frag; /* feat frag image from mli_rgb_fwd */
+  uint16_t* dzT;          /* [4 layers][256][S] */
+  uint16_t* dz4T;         /* [4][S] */
+  float* d_nrm;           /* [N][R][4] scaled d total / d normal (xyz, pad) */
+  uint16_t* dz1T;         /* [256][S] feature-major dZ1sdf (scaled) */
+  uint16_t* dh0_frag;     /* [S/32][16][64][8] d h0 (scaled, layer-1 path only) */
+} mli_geo_bwd_args;
+int mli_geo_bwd(const mli_geo_bwd_args* a, mli_stream_t s);
+
+/* SDF layer 0 + sdf head backward for the 5 points of every sample (center + 4 taps):
+ * combines d sdf / d grad (composite), eikonal / curvature gradients, the normalize
+ * backward of d normal and the tap stencils into d sdf_i; recomputes layer 0 of every point
+ * from the FIELD encodings; writes d enc (fp32, for mli_hash_bwd), dZ0 frag images and the
+ * p rows of the layer-0 input (for the dW GEMM) and accumulates dW/db of linear_sdf. */
+typedef struct {
+  int R, N;
+  const float* center; const float* ray_unit; const float* dists;
+  const uint8_t* outside;
+  const float* grad; const float* hess;   /* forward [N][R][3] */
+  const float* d_sdf; const float* d_grad; /* from mli_composite_bwd_geo */
+  const float* d_nrm;     /* [N][R][4] scaled, from mli_geo_bwd */
+  const uint16_t* dh0_frag; /* from mli_geo_bwd */
+  const uint16_t* enc;    /* FIELD encodings [S/32][5][8][64][8] */
+  const void* wsdf;       /* mli_pack_sdf block */
+  const void* wsdf_t;     /* W0_enc^T block (mli_pack_sdf_t) */
+  float eps, grad_den, hess_den;
+  float w_eikonal, w_curvature;  /* loss weights / (R*N) are applied in-kernel */
+  float grad_scale;
+  float* d_enc;           /* [S/32][5][8][64][8] fp32 (unscaled) */
+  uint16_t* dz0_frag;     /* [5][S/32][16][64][8] scaled dZ0 of the 5 points (ACC order) */
+  uint16_t* x0_rows;      /* [131][5S] fp16 layer-0 input rows (p 0..2, enc 3..130); this writes rows 0..2 */
+  float* dw_sdf;          /* [256] scaled, atomics (caller zeroes) */
+  float* db_sdf;          /* [1] scaled, atomics (caller zeroes) */
+} mli_sdf_bwd_args;
+int mli_sdf_bwd(const mli_sdf_bwd_args* a, mli_stream_t s);
+
+/* W0_enc^T fragments (A operand of d enc = W0_enc^T dZ0; rows ordered so each lane half
+ * holds 8 features of one level) -- MLI_SDF_T_PACK_BYTES. */
+typedef struct {
+  const float* v0; const float* g0;   /* linears.0 [256,131] */
+  uint8_t* dst;
+} mli_pack_sdf_t_args;
+#define MLI_SDF_T_PACK_BYTES 65536
+int mli_pack_sdf_t(const mli_pack_sdf_t_args* a, mli_stream_t s);
+
+/* Hash-grid backward: d table[(offset_l + idx) * 8 + f] += w_corner * d enc, for the 5
+ * points of every sample (taps in the center's cell share its corners: one atomic per
+ * corner feature), levels < active_levels.  fp32 atomics into the caller-zeroed grad. */
+typedef struct {
+  int R, N;
+  const float* center; const float* ray_unit; const float* dists;
+  const float* d_enc;     /* from mli_sdf_bwd */
+  mli_grid_levels levels;
+  float eps;
+  int active_levels;
+  float* d_table;         /* [entries*8] fp32 */
+} mli_hash_bwd_args;
+int mli_hash_bwd(const mli_hash_bwd_args* a, mli_stream_t s);
+
+/* Frag image -> feature-major rows: src [tiles][tile_stride halves], k-step q of tile t at
+ * src + t*tile_stride + q*512; element (q, lane half h, j) of sample t*32 + (lane & 31) goes
+ * to row row0 + k(q,h,j) (order 0: NAT 16q+8h+j, 1: ACC) at column col0 + sample. */
+typedef struct {
+  const uint16_t* src;
+  int64_t tile_stride;
+  int tiles, k_steps, order;
+  uint16_t* dst;
+  int64_t ld;             /* row stride (elements) */
+  int64_t col0;
+  int row0;
+} mli_frag_rows_args;
+int mli_frag_rows(const mli_frag_rows_args* a, mli_stream_t s);
+
 /* ---------------------------------------------------------------- losses
  * Stage-b loss terms and d(total)/d(rgb, o_r, o_s, o_re) in one call (three launches):
  * replaces NeuralLumen/trainer.py:133-149 (_compute_loss) with eikonal/curvature
@@ -271,6 +386,8 @@ typedef struct {
   const uint8_t* kmode;   /* [k_steps] 0: NAT, 1: ACC ordering                             */
   int64_t dst_offset;     /* byte offset of the first chunk in dst                         */
   int chunk_stride;       /* bytes per chunk (k_steps*1024 + 128)                          */
+  const int16_t* nmap;    /* transpose only: [n_tiles*32] packed row -> W column (-1: zero);
+                             NULL: identity                                                 */
 } mli_pack_layer;
 typedef struct {
   int n_layers;
@@ -298,6 +415,7 @@ typedef struct {
   const int16_t* kinv;    /* [k_ref] reference column -> packed k                         */
   float* grad_v; float* grad_g; float* grad_b;
   const float* extra_db;  /* NULL */
+  int plain;              /* 1: plain Linear (no weight norm): grad_v = dW * inv_scale */
 } mli_assemble_layer;
 typedef struct {
   int n_layers;
@@ -313,6 +431,7 @@ typedef struct {
   int64_t n;
   float lr, beta1, beta2, eps, weight_decay;
   int step;               /* 1-based step after increment */
+  uint16_t* p16;          /* optional fp16 copy of the updated p (hash-table shadow), or NULL */
 } mli_adamw_args;
 int mli_adamw(const mli_adamw_args* a, mli_stream_t s);
 

@@ -34,7 +34,7 @@ class SdfArgs(C.Structure):
                 ("dists", P), ("outside", P), ("table", P), ("levels", GridLevels), ("wsdf", P),
                 ("eps", F32), ("grad_den", F32), ("hess_den", F32), ("outside_val", F32),
                 ("with_hessian", I32), ("sdf", P), ("grad", P), ("hess", P), ("h0", P),
-                ("enc", P)]
+                ("enc", P), ("active_levels", I32)]
 
 
 class SampleCoarseArgs(C.Structure):
@@ -50,7 +50,7 @@ class SampleFineArgs(C.Structure):
 class RgbFwdArgs(C.Structure):
     _fields_ = [("R", I32), ("N", I32), ("center", P), ("ray_unit", P), ("pts_light", P),
                 ("dists", P), ("grad", P), ("h0", P), ("wfwd", P), ("y", P), ("feat_frag", P),
-                ("x0T", P), ("xT", P), ("masks", P)]
+                ("x0T", P), ("xT", P), ("masks", P), ("n_heads", I32)]
 
 
 class CompositeArgs(C.Structure):
@@ -92,7 +92,7 @@ class LossArgs(C.Structure):
 class PackLayer(C.Structure):
     _fields_ = [("v", P), ("g", P), ("bias", P), ("n_out", I32), ("k_ref", I32), ("transpose", I32),
                 ("n_tiles", I32), ("k_steps", I32), ("kmap", P), ("kmode", P), ("dst_offset", I64),
-                ("chunk_stride", I32)]
+                ("chunk_stride", I32), ("nmap", P)]
 
 
 class PackArgs(C.Structure):
@@ -106,7 +106,7 @@ class PackSdfArgs(C.Structure):
 class AssembleLayer(C.Structure):
     _fields_ = [("dw", P), ("db", P), ("v", P), ("g", P), ("n_out", I32), ("k_ref", I32),
                 ("k_pack", I32), ("kinv", P), ("grad_v", P), ("grad_g", P), ("grad_b", P),
-                ("extra_db", P)]
+                ("extra_db", P), ("plain", I32)]
 
 
 class AssembleArgs(C.Structure):
@@ -115,14 +115,47 @@ class AssembleArgs(C.Structure):
 
 class AdamwArgs(C.Structure):
     _fields_ = [("p", P), ("g", P), ("m", P), ("v", P), ("n", I64), ("lr", F32), ("beta1", F32),
-                ("beta2", F32), ("eps", F32), ("weight_decay", F32), ("step", I32)]
+                ("beta2", F32), ("eps", F32), ("weight_decay", F32), ("step", I32), ("p16", P)]
 
 
 class CastArgs(C.Structure):
     _fields_ = [("src", P), ("dst", P), ("n", I64)]
 
 
-ABI_VERSION = 5  # include/mli_hip.h MLI_ABI_VERSION
+class CompositeBwdGeoArgs(C.Structure):
+    _fields_ = [("R", I32), ("N", I32), ("dists", P), ("far_", P), ("ray_unit", P), ("sdf", P), ("grad", P),
+                ("y", P), ("s_var", P), ("anneal", F32), ("white_bg", I32), ("d_rgb", P), ("grad_scale", F32),
+                ("dz4", P), ("d_sdf", P), ("d_grad", P), ("d_inv_s_acc", P), ("d_s_var", P)]
+
+
+class GeoBwdArgs(C.Structure):
+    _fields_ = [("R", I32), ("N", I32), ("dz4", P), ("wgeo", P), ("masks", P), ("feat_frag", P), ("dzT", P),
+                ("dz4T", P), ("d_nrm", P), ("dz1T", P), ("dh0_frag", P)]
+
+
+class SdfBwdArgs(C.Structure):
+    _fields_ = [("R", I32), ("N", I32), ("center", P), ("ray_unit", P), ("dists", P), ("outside", P),
+                ("grad", P), ("hess", P), ("d_sdf", P), ("d_grad", P), ("d_nrm", P), ("dh0_frag", P), ("enc", P),
+                ("wsdf", P), ("wsdf_t", P), ("eps", F32), ("grad_den", F32), ("hess_den", F32),
+                ("w_eikonal", F32), ("w_curvature", F32), ("grad_scale", F32), ("d_enc", P), ("dz0_frag", P),
+                ("x0_rows", P), ("dw_sdf", P), ("db_sdf", P)]
+
+
+class PackSdfTArgs(C.Structure):
+    _fields_ = [("v0", P), ("g0", P), ("dst", P)]
+
+
+class HashBwdArgs(C.Structure):
+    _fields_ = [("R", I32), ("N", I32), ("center", P), ("ray_unit", P), ("dists", P), ("d_enc", P),
+                ("levels", GridLevels), ("eps", F32), ("active_levels", I32), ("d_table", P)]
+
+
+class FragRowsArgs(C.Structure):
+    _fields_ = [("src", P), ("tile_stride", I64), ("tiles", I32), ("k_steps", I32), ("order", I32), ("dst", P),
+                ("ld", I64), ("col0", I64), ("row0", I32)]
+
+
+ABI_VERSION = 6  # include/mli_hip.h MLI_ABI_VERSION
 
 ENTRY_POINTS = {
     "mli_rays": RaysArgs, "mli_hashgrid_fwd": HashgridArgs, "mli_sdf": SdfArgs,
@@ -131,6 +164,8 @@ ENTRY_POINTS = {
     "mli_composite_bwd": CompositeBwdArgs, "mli_rgb_bwd": RgbBwdArgs, "mli_wgrad": WgradArgs,
     "mli_pack": PackArgs, "mli_pack_sdf": PackSdfArgs, "mli_grad_assemble": AssembleArgs,
     "mli_adamw": AdamwArgs, "mli_cast_f16": CastArgs, "mli_stage_b_loss": LossArgs,
+    "mli_composite_bwd_geo": CompositeBwdGeoArgs, "mli_geo_bwd": GeoBwdArgs, "mli_sdf_bwd": SdfBwdArgs,
+    "mli_pack_sdf_t": PackSdfTArgs, "mli_hash_bwd": HashBwdArgs, "mli_frag_rows": FragRowsArgs,
 }
 
 _lib = None

@@ -57,6 +57,10 @@ PRESETS = {
     "syn_hotdog_b": {},
     "NRHints_Pikachu_b": {"model": {"background": {"white": False}},
                           "data": {"white_background": False}},
+    # stage a (syn_hotdog_a.yaml): LumenRGB mode 'rgb' (no network_mode), coarse-to-fine from
+    # 8 active levels, render/eikonal/curvature losses only, every parameter trained
+    "syn_hotdog_a": {"model": {"object": {"sdf": {"encoding": {"coarse2fine": {"enabled": True,
+                                                                                "init_active_level": 8}}}}}},
     "rene_savannah_b": {"model": {"background": {"white": False}},
                         "data": {"bounding_type": "box", "white_background": False,
                                  "bounding_box_aabb": [-0.66, -0.516, -0.18, 0.66, 0.42, 0.3],
@@ -64,10 +68,28 @@ PRESETS = {
 }
 
 
+# keys a preset removes from BASE (the stage-b additions the stage-a YAMLs do not have)
+DROP = {
+    "syn_hotdog_a": ("model.object.rgb.network_mode", "model.object.rgb.shading_dim", "trainer.partial_grad",
+                     "optim.partial_training", "trainer.loss_weight.intrinsic",
+                     "trainer.loss_weight.regularize_re"),
+}
+
+
+def _drop(cfg, path):
+    keys = path.split(".")
+    node = cfg
+    for k in keys[:-1]:
+        node = node[k]
+    node.pop(keys[-1], None)
+
+
 def preset(name="syn_hotdog_b", rays=None, n_coarse=None, n_fine=None, n_hier=None, log2T=None,
            overrides=None):
     cfg = copy.deepcopy(BASE)
     merge(cfg, copy.deepcopy(PRESETS[name]))
+    for path in DROP.get(name, ()):
+        _drop(cfg, path)
     r = cfg["model"]["render"]
     if rays is not None:
         r["rand_rays"] = rays

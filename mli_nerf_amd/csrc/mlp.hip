@@ -180,7 +180,6 @@ struct NoPre {
 // chunk sizes in consumption order: SDF layer 1 (8 x KS 16), then per head L0 (8 x KS 19),
 // L1..L3 (24 x KS 16), L4 (1 x KS 16)
 MLI_FI int fwd_bytes(int c) { return (c >= 8 && (c - 8) % 33 < 8) ? CH(19) : CH(16); }
-constexpr int FWD_CHUNKS = 8 + 3 * 33;
 
 template <bool TRAIN>
 __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
@@ -195,7 +194,7 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
   auto bytes = [](int cc) MLI_LAMBDA_FI { return fwd_bytes(cc); };
 
   Ring rg;
-  ring_start(rg, a.wfwd, FWD_CHUNKS, bytes);
+  ring_start(rg, a.wfwd, 8 + a.n_heads * 33, bytes);
 
   half8 A[16], B[19];
   // h0 frags (SDF layer-0 activations) -> B[0..15]
@@ -263,7 +262,7 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
     if (TRAIN) stage_tile(sg, lds, v, a.x0T + (size_t)(32 * t) * S + col0, lane);
   });
 
-  for (int hd = 0; hd < 3; ++hd) {
+  for (int hd = 0; hd < a.n_heads; ++hd) {
     const int S = opaque_s(a.R * a.N);
     // reload feat frags into B[0..15] (B[16..18] keep the extras); the lane offset is made
     // opaque per head so the 16 addresses are not hoisted out of the head loop (spills)
@@ -402,6 +401,141 @@ __global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
   vm_wait(0);
 }
 
+
+// ---------------------------------------------------------------------- stage a: geometry dX chain
+// The single 'rgb' head (NeuralLumen/utils/modules.py:164-174) backward down to its inputs,
+// then SDF layer 1.  Chunks: W4^T (8 x KS 1), W3^T, W2^T, W1^T (24 x KS 16), W0^T (9 n-tiles
+// over packed input rows 0..287: feat (ACC order) + the p/normal k-step), W1sdf^T (8 x KS 16).
+MLI_FI int geo_bytes(int c) { return c < 8 ? CH(1) : CH(16); }
+constexpr int GEO_CHUNKS = 8 + 24 + 9 + 8;
+
+__global__ __launch_bounds__(THREADS) void geo_bwd_kernel(mli_geo_bwd_args a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int S = a.R * a.N;
+  const int tiles = S / 32;
+  const int tile = blockIdx.x * WAVES + wave;
+  const int m = tile * 32 + c;
+  const int r = m / a.N, k = m - r * a.N;
+  const size_t slot = (size_t)k * a.R + r;
+  auto bytes = [](int cc) MLI_LAMBDA_FI { return geo_bytes(cc); };
+  // ReLU-mask block of head layer 3 - L (L = 0..3), one 16 B DMA per thread into slot L & 1
+  auto mask_dma = [&](int L) MLI_LAMBDA_FI {
+    const int ml = 3 - min(L, 3);
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(a.masks) +
+                         (((size_t)ml * tiles + (size_t)blockIdx.x * WAVES) * 64) * 16;
+    glds16(src + threadIdx.x * 16, lds + MASK_OFF + (L & 1) * 8192 + wave * 1024);
+  };
+
+  Ring rg;
+  ring_start(rg, a.wgeo, GEO_CHUNKS, bytes);
+  mask_dma(0);
+#pragma unroll
+  for (int d = 0; d < DIST; ++d) ring_issue(rg, lds, bytes);
+  vm_wait((DIST - 1) * GLDS);
+  block_sync();
+
+  half8 A[16], B[16];
+  Stager sg{nullptr, 0, 0};
+  const size_t col0 = (size_t)blockIdx.x * 256;
+  half8 z4;
+  {
+    const float* dz = a.dz4 + 8 * slot;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z4[j] = (f16)0.f;
+    if (h == 0) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const f16 zj = (f16)dz[j];
+        z4[j] = zj;
+        a.dz4T[(size_t)j * S + m] = __builtin_bit_cast(uint16_t, zj);
+      }
+    }
+  }
+  struct MaskPre {
+    decltype(mask_dma)& dma;
+    int next_layer;
+    MLI_FI int count(int t) const { return t == 8 - DIST ? 1 : 0; }
+    MLI_FI void issue(int t) const {
+      if (t == 8 - DIST) dma(next_layer);
+    }
+  };
+  auto pre = [&](int li) MLI_LAMBDA_FI { return MaskPre{mask_dma, li + 1}; };
+  auto mask_epi = [&](half8* out, int layer, int li) MLI_LAMBDA_FI {
+    return [&, out, layer, li](int t, const f32x16& acc) MLI_LAMBDA_FI {
+      const u32x4 mv =
+          *reinterpret_cast<const u32x4*>(lds + MASK_OFF + (li & 1) * 8192 + wave * 1024 + lane * 16);
+      const int wi = t >> 1;
+      const uint32_t word = wi == 0 ? mv[0] : wi == 1 ? mv[1] : wi == 2 ? mv[2] : mv[3];
+      const uint32_t bits = word >> ((t & 1) * 16);
+      f32x16 v;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = ((bits >> i) & 1u) ? acc[i] : 0.0f;
+      out[2 * t] = acc_to_frag(v, 0);
+      out[2 * t + 1] = acc_to_frag(v, 1);
+      stage_tile(sg, lds, v, a.dzT + ((size_t)layer * 256 + 32 * t) * S + col0, lane);
+    };
+  };
+  run_layer<1, 8, true, 0, false>(rg, lds, sg, S, &z4, lane, bytes, pre(0), mask_epi(A, 3, 0));
+  run_layer<16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, pre(1), mask_epi(B, 2, 1));
+  run_layer<16, 8, true, 0, false>(rg, lds, sg, S, B, lane, bytes, pre(2), mask_epi(A, 1, 2));
+  run_layer<16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, NoPre{}, mask_epi(B, 0, 3));
+  // feat frags (softplus output of SDF layer 1, forward scratch), one tile ahead of its use:
+  // tile 0 now, tile t+1 ahead of phase t's weight DMAs (counted as pre-issued VMEM ops)
+  const half8* fsrc = reinterpret_cast<const half8*>(a.feat_frag + (size_t)tile * FRAG_TILE) + lane;
+  half8 F[2][2];
+  F[0][0] = fsrc[0];
+  F[0][1] = fsrc[64];
+  struct FeatPre {
+    const half8* src;
+    half8 (&F)[2][2];
+    MLI_FI int count(int t) const { return t < 7 ? 2 : 0; }
+    MLI_FI void issue(int t) const {
+      if (t < 7) {
+        F[(t + 1) & 1][0] = src[(2 * t + 2) * 64];
+        F[(t + 1) & 1][1] = src[(2 * t + 3) * 64];
+      }
+    }
+  };
+  // dX0 = W0^T dZ0: tiles 0..7 = d feat -> dZ1sdf = d feat * softplus'(z1), with
+  // softplus'(z1) = 1 - exp(-100 feat) (torch: z/(z+1), z = e^{100 z1}; 1 past the threshold);
+  // tile 8 = rows 256..287 (p 256..258, normal 259..261: (i=3,h=0), (i=0,h=1), (i=1,h=1))
+  run_layer<16, 9, true, 0, false>(rg, lds, sg, S, B, lane, bytes, FeatPre{fsrc, F},
+                                   [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
+    if (t < 8) {
+      f32x16 v;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = (float)F[t & 1][s2][j];
+          v[8 * s2 + j] = acc[8 * s2 + j] * (1.0f - __expf(-100.0f * f));
+        }
+      A[2 * t] = acc_to_frag(v, 0);
+      A[2 * t + 1] = acc_to_frag(v, 1);
+      stage_tile(sg, lds, v, a.dz1T + (size_t)(32 * t) * S + col0, lane);
+    } else {
+      float* dn = a.d_nrm + 4 * slot;
+      if (h == 0) {
+        dn[0] = acc[3];
+      } else {
+        dn[1] = acc[0];
+        dn[2] = acc[1];
+      }
+    }
+  });
+  // d h0 (layer-1 path) = W1sdf^T dZ1sdf -> frag image (ACC order, as the h0 image)
+  uint16_t* dtile = a.dh0_frag + (size_t)tile * FRAG_TILE;
+  run_layer<16, 8, false, 2, false>(rg, lds, sg, S, A, lane, bytes, NoPre{},
+                                    [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
+    half8* dst = reinterpret_cast<half8*>(dtile) + (2 * t) * 64 + lane;
+    __builtin_nontemporal_store(acc_to_frag(acc, 0), dst);
+    __builtin_nontemporal_store(acc_to_frag(acc, 1), dst + 64);
+  });
+  vm_wait(0);
+}
+
 }  // namespace
 
 extern "C" int mli_rgb_fwd(const mli_rgb_fwd_args* a, mli_stream_t s) {
@@ -409,6 +543,7 @@ extern "C" int mli_rgb_fwd(const mli_rgb_fwd_args* a, mli_stream_t s) {
   if (S % 256 != 0) return (int)hipErrorInvalidValue;
   const bool train = a->xT != nullptr;
   if (train && (a->x0T == nullptr || a->masks == nullptr)) return (int)hipErrorInvalidValue;
+  if (a->n_heads != 1 && a->n_heads != 3) return (int)hipErrorInvalidValue;
   if (train)
     hipLaunchKernelGGL(rgb_fwd_kernel<true>, dim3(S / 256), dim3(THREADS), LDS_FWD, (hipStream_t)s, *a);
   else
@@ -420,5 +555,15 @@ extern "C" int mli_rgb_bwd(const mli_rgb_bwd_args* a, mli_stream_t s) {
   const int S = a->R * a->N;
   if (S % 256 != 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(rgb_bwd_kernel, dim3(S / 256), dim3(THREADS), LDS_BWD, (hipStream_t)s, *a);
+  MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_geo_bwd(const mli_geo_bwd_args* a, mli_stream_t s) {
+  const int S = a->R * a->N;
+  if (S % 256 != 0) return (int)hipErrorInvalidValue;
+  if (!a->dz4 || !a->wgeo || !a->masks || !a->feat_frag || !a->dzT || !a->dz4T || !a->d_nrm || !a->dz1T ||
+      !a->dh0_frag)
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(geo_bwd_kernel, dim3(S / 256), dim3(THREADS), LDS_BWD, (hipStream_t)s, *a);
   MLI_LAUNCH_CHECK();
 }

@@ -54,8 +54,9 @@ __global__ __launch_bounds__(256) void pack_kernel(const mli_pack_layer* layers,
       if (!L.transpose) {
         if (n < rows_src) w = L.v[(size_t)n * cols_src + src] * sc_row;
       } else {
-        // A = W^T: row n indexes W's columns, packed k indexes W's rows (src)
-        if (n < cols_src) w = L.v[(size_t)src * cols_src + n] * rs[src];
+        // A = W^T: row n indexes W's columns (through nmap), packed k indexes W's rows (src)
+        const int col = L.nmap ? L.nmap[n] : (n < cols_src ? n : -1);
+        if (col >= 0) w = L.v[(size_t)src * cols_src + col] * rs[src];
       }
     }
     out[j] = (f16)w;
@@ -73,6 +74,12 @@ __global__ __launch_bounds__(256) void assemble_kernel(const mli_assemble_layer*
   if (n >= L.n_out) return;
   __shared__ float red[2][256];
   const int tid = threadIdx.x;
+  if (L.plain) {  // plain nn.Linear (linear_sdf, mlp.py:50): no weight-norm backward
+    for (int c = tid; c < L.k_ref; c += 256)
+      L.grad_v[(size_t)n * L.k_ref + c] = L.dw[(size_t)n * L.k_pack + L.kinv[c]] * inv_scale;
+    if (tid == 0) L.grad_b[n] = L.db[n] * inv_scale;
+    return;
+  }
   const float* vr = L.v + (size_t)n * L.k_ref;
   float ss = 0.f, dot = 0.f;
   for (int c = tid; c < L.k_ref; c += 256) {
@@ -118,6 +125,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(mli_adamw_args a, float bc1,
   a.p[i] = p;
   a.m[i] = m;
   a.v[i] = v;
+  if (a.p16) a.p16[i] = __builtin_bit_cast(uint16_t, (f16)p);  // fp16 gather shadow (hash table)
 }
 
 __global__ __launch_bounds__(256) void cast_kernel(mli_cast_args a) {

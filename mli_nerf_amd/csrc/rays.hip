@@ -400,6 +400,112 @@ __global__ __launch_bounds__(256) void composite_bwd_kernel(mli_composite_bwd_ar
   *reinterpret_cast<f32x4*>(a.dz4 + 8 * s + 4) = o1;
 }
 
+
+// Stage-a composite backward (geometry terms), one wave per ray, lane l owning samples
+// 4l..4l+3.  The forward alphas are recomputed with the forward kernel's arithmetic; the
+// transmittance backward uses the suffix recurrence
+//   B_k = sum_{j>k} dw_j a_j prod_{k<m<j} (1 - a_m) = dw_{k+1} a_{k+1} + (1 - a_{k+1}) B_{k+1},
+//   d a_k = T_k (dw_k - B_k)
+// (division-free, exact where 1 - a = 0), evaluated as a wave suffix scan of affine maps.
+// Then clamp (torch: inclusive bounds), the NeuS ratio, the two sigmoids, the section
+// endpoints (d sdf, d iter_cos, d inv_s) and _get_iter_cos (relu' = [x > 0]) -> d grad.
+__global__ __launch_bounds__(CW * 64) void composite_bwd_geo_kernel(mli_composite_bwd_geo_args a) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int R = a.R, N = a.N;
+  const int r = blockIdx.x * CW + w;
+  if (r >= R) return;
+  const float inv_s = expf(a.s_var[0]);
+  const float an = a.anneal;
+  const float v0 = a.ray_unit[3 * r], v1 = a.ray_unit[3 * r + 1], v2 = a.ray_unit[3 * r + 2];
+  const float far = a.far_[r];
+  const float dr0 = a.d_rgb[3 * r], dr1 = a.d_rgb[3 * r + 1], dr2 = a.d_rgb[3 * r + 2];
+  const float bg = a.white_bg ? (dr0 + dr1) + dr2 : 0.f;  // rgb += 1 - sum(w)
+  constexpr int E = 4;
+  float al[E], x[E], cp[E], cn[E], ep[E], en[E], st[E], cs[E], dw[E], yv[E][3];
+  float lp = 1.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int k = E * lane + e;
+    al[e] = 0.f; x[e] = 0.f; cp[e] = cn[e] = 0.5f; ep[e] = en[e] = 0.f; st[e] = 0.f; cs[e] = 0.f; dw[e] = 0.f;
+    yv[e][0] = yv[e][1] = yv[e][2] = 0.f;
+    if (k < N) {
+      const size_t s = (size_t)k * R + r;
+      const float dk = a.dists[s];
+      const float dn = (k + 1 < N) ? a.dists[s + R] : far;
+      st[e] = dn - dk;
+      const float g0 = a.grad[3 * s], g1 = a.grad[3 * s + 1], g2 = a.grad[3 * s + 2];
+      cs[e] = (v0 * g0 + v1 * g1) + v2 * g2;
+      const float ic = -(fmaxf(-cs[e] * 0.5f + 0.5f, 0.f) * (1.0f - an) + fmaxf(-cs[e], 0.f) * an);
+      const float sd = a.sdf[s];
+      ep[e] = sd - (ic * st[e]) * 0.5f;
+      en[e] = sd + (ic * st[e]) * 0.5f;
+      cp[e] = 1.0f / (1.0f + expf(-(ep[e] * inv_s)));
+      cn[e] = 1.0f / (1.0f + expf(-(en[e] * inv_s)));
+      x[e] = (cp[e] - cn[e]) / (cp[e] + 1e-5f);
+      al[e] = fminf(fmaxf(x[e], 0.f), 1.f);
+      const f32x4 y0 = *reinterpret_cast<const f32x4*>(a.y + 8 * s);
+      yv[e][0] = y0[0]; yv[e][1] = y0[1]; yv[e][2] = y0[2];
+      dw[e] = ((dr0 * y0[0] + dr1 * y0[1]) + dr2 * y0[2]) - bg;
+    }
+    lp *= 1.0f - al[e];
+  }
+  float T[E];
+  T[0] = wave_excl_prod(lp, lane);
+#pragma unroll
+  for (int e = 1; e < E; ++e) T[e] = T[e - 1] * (1.0f - al[e - 1]);
+  // this lane's map B_in -> B_{4l-1}: f_{4l} o ... o f_{4l+3}, f_j(x) = (1 - a_j) x + dw_j a_j
+  float ma = 1.f, mb = 0.f;
+#pragma unroll
+  for (int e = E - 1; e >= 0; --e) {
+    mb = (1.0f - al[e]) * mb + dw[e] * al[e];
+    ma = (1.0f - al[e]) * ma;
+  }
+  // suffix scan: G_l = F_l o F_{l+1} o ... o F_63
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float na = __shfl_down(ma, o), nb = __shfl_down(mb, o);
+    if (lane + o < 64) { mb = ma * nb + mb; ma = ma * na; }
+  }
+  float B = __shfl_down(mb, 1);
+  if (lane == 63) B = 0.f;
+  float dinv = 0.f;
+#pragma unroll
+  for (int e = E - 1; e >= 0; --e) {
+    const int k = E * lane + e;
+    const float da = T[e] * (dw[e] - B);
+    B = (1.0f - al[e]) * B + dw[e] * al[e];
+    if (k >= N) continue;
+    const size_t s = (size_t)k * R + r;
+    const float dx = (x[e] >= 0.f && x[e] <= 1.f) ? da : 0.f;
+    const float den_ = cp[e] + 1e-5f;
+    const float dcp = dx * (1.0f - x[e]) / den_, dcn = -dx / den_;
+    const float dtp = dcp * (cp[e] * (1.0f - cp[e])), dtn = dcn * (cn[e] * (1.0f - cn[e]));
+    const float dep = dtp * inv_s, den = dtn * inv_s;
+    dinv += dtp * ep[e] + dtn * en[e];
+    a.d_sdf[s] = dep + den;
+    const float dic = (den - dep) * 0.5f * st[e];
+    const float dcos = dic * ((-cs[e] * 0.5f + 0.5f > 0.f ? 0.5f * (1.0f - an) : 0.f) + (-cs[e] > 0.f ? an : 0.f));
+    a.d_grad[3 * s] = v0 * dcos;
+    a.d_grad[3 * s + 1] = v1 * dcos;
+    a.d_grad[3 * s + 2] = v2 * dcos;
+    const float wsc = al[e] * T[e] * a.grad_scale;
+    f32x4 o0, o1;
+    o0[0] = wsc * dr0 * (yv[e][0] * (1.f - yv[e][0]));
+    o0[1] = wsc * dr1 * (yv[e][1] * (1.f - yv[e][1]));
+    o0[2] = wsc * dr2 * (yv[e][2] * (1.f - yv[e][2]));
+    o0[3] = 0.f;
+    o1[0] = o1[1] = o1[2] = o1[3] = 0.f;
+    *reinterpret_cast<f32x4*>(a.dz4 + 8 * s) = o0;
+    *reinterpret_cast<f32x4*>(a.dz4 + 8 * s + 4) = o1;
+  }
+  dinv = wave_sum(dinv);
+  if (lane == 0) unsafeAtomicAdd(a.d_inv_s_acc, dinv);
+}
+
+__global__ void svar_grad_kernel(mli_composite_bwd_geo_args a) {
+  a.d_s_var[0] = expf(a.s_var[0]) * a.d_inv_s_acc[0];  // inv_s = exp(s_var)
+}
+
 }  // namespace
 
 extern "C" int mli_rays(const mli_rays_args* a, mli_stream_t s) {
@@ -437,5 +543,13 @@ extern "C" int mli_composite_bwd(const mli_composite_bwd_args* a, mli_stream_t s
   if (a->R <= 0) return 0;
   const size_t S = (size_t)a->R * a->N;
   hipLaunchKernelGGL(composite_bwd_kernel, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, (hipStream_t)s, *a);
+  MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_composite_bwd_geo(const mli_composite_bwd_geo_args* a, mli_stream_t s) {
+  if (a->R <= 0) return 0;
+  if (a->N > 256) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(composite_bwd_geo_kernel, dim3((a->R + CW - 1) / CW), dim3(CW * 64), 0, (hipStream_t)s, *a);
+  hipLaunchKernelGGL(svar_grad_kernel, dim3(1), dim3(1), 0, (hipStream_t)s, *a);
   MLI_LAUNCH_CHECK();
 }

@@ -63,17 +63,24 @@ MLI_FI void load_rowc(const uint8_t* lds, int arr, int t, int h, float (&v)[16])
 
 // Hash encoding of one point per lane (both lane halves see the same point; half h holds
 // level 2q+h of k-step q): the B-fragment image X0^T of layer 0, NAT order.
-MLI_FI void hash_encode(const uint16_t* __restrict__ table, const mli_grid_levels& L, int lane, float px,
-                        float py, float pz, half8 (&enc)[8]) {
+MLI_FI void hash_encode(const uint16_t* __restrict__ table, const mli_grid_levels& L, int active, int lane,
+                        float px, float py, float pz, half8 (&enc)[8]) {
   const int h = lane >> 5;
   // x01 = (p - (-2)) / (2 - (-2))  (modules.py:82-83)
   const float x0 = (px + 2.0f) * 0.25f, x1 = (py + 2.0f) * 0.25f, x2 = (pz + 2.0f) * 0.25f;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
+    // coarse-to-fine mask (modules.py:91-93): levels >= active encode to 0 (uniform branch)
+    if (2 * q >= active) {
+#pragma unroll
+      for (int f = 0; f < 8; ++f) enc[q][f] = (f16)0.0f;
+      continue;
+    }
     float acc[8];
     hash_level_pair(table, L, 2 * q, 2 * q + 1, h, x0, x1, x2, acc);
+    const bool keep = 2 * q + h < active;
 #pragma unroll
-    for (int f = 0; f < 8; ++f) enc[q][f] = (f16)acc[f];
+    for (int f = 0; f < 8; ++f) enc[q][f] = (f16)(keep ? acc[f] : 0.0f);
     // at most two levels (16 x 16 B gathers) in flight per lane
     if (q & 1) __builtin_amdgcn_sched_barrier(0);
   }
@@ -118,9 +125,9 @@ MLI_FI float sdf_from_enc(const uint8_t* lds, const half8 (&enc)[8], int lane, f
 }
 
 MLI_FI float sdf_point(const uint8_t* lds, const uint16_t* __restrict__ table, const mli_grid_levels& L,
-                       int lane, float px, float py, float pz, uint16_t* __restrict__ h0_tile) {
+                       int active, int lane, float px, float py, float pz, uint16_t* __restrict__ h0_tile) {
   half8 enc[8];
-  hash_encode(table, L, lane, px, py, pz, enc);
+  hash_encode(table, L, active, lane, px, py, pz, enc);
   return sdf_from_enc(lds, enc, lane, px, py, pz, h0_tile);
 }
 
@@ -133,7 +140,7 @@ MLI_FI float sdf_point(const uint8_t* lds, const uint16_t* __restrict__ table, c
 constexpr int TAPS = 5;
 
 template <int KIND>
-MLI_FI void level5(const uint16_t* __restrict__ table, const LevelP& P, const float (&x)[TAPS][3],
+MLI_FI void level5(const uint16_t* __restrict__ table, const LevelP& P, const float (&x)[TAPS][3], bool keep,
                    uint16_t* __restrict__ dst /* enc + (tile*5*8 + q)*512 + lane*8 */) {
   const uint32_t r2 = P.res * P.res;
   const bool dense_lane = (uint64_t)P.res * P.res * P.res <= (uint64_t)P.size;
@@ -173,7 +180,7 @@ MLI_FI void level5(const uint16_t* __restrict__ table, const LevelP& P, const fl
     }
     half8 e;
 #pragma unroll
-    for (int f = 0; f < 8; ++f) e[f] = (f16)acc[f];
+    for (int f = 0; f < 8; ++f) e[f] = (f16)(keep ? acc[f] : 0.0f);  // c2f mask
     *reinterpret_cast<half8*>(out) = e;
   };
   // center
@@ -255,12 +262,18 @@ __global__ __launch_bounds__(256) void encode5_kernel(mli_sdf_args a, int tile0,
                    h ? P1.offset : P0.offset, h ? P1.magic : P0.magic};
     const bool d0 = level_dense(L, lv0), d1 = level_dense(L, lv1);
     uint16_t* dst = base + (size_t)qq * 512;
+    if (lv0 >= a.active_levels) {  // coarse-to-fine: the whole level pair encodes to 0
+#pragma unroll
+      for (int p = 0; p < TAPS; ++p) *reinterpret_cast<u32x4*>(dst + (size_t)p * 8 * 512) = u32x4{0, 0, 0, 0};
+      continue;
+    }
+    const bool keep = (h ? lv1 : lv0) < a.active_levels;
     if (d0 && d1)
-      level5<0>(a.table, P, x, dst);
+      level5<0>(a.table, P, x, keep, dst);
     else if (!d0 && !d1)
-      level5<1>(a.table, P, x, dst);
+      level5<1>(a.table, P, x, keep, dst);
     else
-      level5<2>(a.table, P, x, dst);
+      level5<2>(a.table, P, x, keep, dst);
   }
 }
 
@@ -349,7 +362,7 @@ __global__ __launch_bounds__(256) void sdf_kernel(mli_sdf_args a) {
     const float px = __fadd_rn(a.center[3 * r + 0], __fmul_rn(a.ray_unit[3 * r + 0], d));
     const float py = __fadd_rn(a.center[3 * r + 1], __fmul_rn(a.ray_unit[3 * r + 1], d));
     const float pz = __fadd_rn(a.center[3 * r + 2], __fmul_rn(a.ray_unit[3 * r + 2], d));
-    const float s = sdf_point(lds_t, a.table, a.levels, lane, px, py, pz, nullptr);
+    const float s = sdf_point(lds_t, a.table, a.levels, a.active_levels, lane, px, py, pz, nullptr);
     if (valid && h == 0) a.sdf[slot] = s;
   }
 }
@@ -407,6 +420,353 @@ __global__ __launch_bounds__(256) void pack_sdf_kernel(mli_pack_sdf_args a) {
   }
 }
 
+
+// ================================================================ stage a: backward
+// W0_enc^T block: 4 n-tiles x 16 k-steps of A fragments.  Row r of n-tile u holds the
+// layer-0 weights of encoding feature (level 2q'+h, feature f) with h = (r>>2)&1,
+// i = (r&3) + 4(r>>3), q' = 2u + (i>>3), f = i&7, so accumulator register i of lane half h is
+// that feature; k = h0 index in ACC order (the dZ0 fragments come from acc_to_frag).
+constexpr int SDFT_PIECES = MLI_SDF_T_PACK_BYTES / 16;
+__global__ __launch_bounds__(256) void pack_sdf_t_kernel(mli_pack_sdf_t_args a) {
+  // blockIdx.x = (u*16 + q); thread = lane*8 + j (512 elements per k-step)... 64 lanes x 8
+  const int uq = blockIdx.x, u = uq >> 4, q = uq & 15;
+  for (int e = threadIdx.x; e < 512; e += blockDim.x) {
+    const int lane = e >> 3, j = e & 7;
+    const int rl = lane & 31, hh = lane >> 5;
+    const int hr = (rl >> 2) & 1, i = (rl & 3) + 4 * (rl >> 3);
+    const int qp = 2 * u + (i >> 3), level = 2 * qp + hr, f = i & 7;
+    const int col = 3 + level * 8 + f;
+    const int n = k_acc(q, hh, j);  // h0 index = output row of W0
+    const float* vrow = a.v0 + n * 131;
+    float ss = 0.f;
+    for (int kk = 0; kk < 131; ++kk) ss += vrow[kk] * vrow[kk];
+    const float w = vrow[col] * (a.g0[n] / sqrtf(ss));
+    reinterpret_cast<f16*>(a.dst + uq * 1024 + lane * 16)[j] = (f16)w;
+  }
+}
+
+MLI_FI void load_block(uint8_t* lds, const void* src_v, int pieces) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(src_v);
+  for (int base = wave * 64; base < pieces; base += nw * 64) {
+    const int piece = min(base + lane, pieces - 1);
+    glds16(src + piece * 16, lds + base * 16);
+  }
+}
+
+// Sum of v[0..15] over the 32 lanes of each lane half (samples), by recursive halving: lane c
+// ends with the total of register i = (c >> 1) & 15 (lanes c, c^1 both hold it).
+MLI_FI float half_reduce16(const float (&v)[16], int c) {
+  float p8[8], p4[4], p2[2];
+  // bitwise selects (a ternary on the arrays becomes a dynamically indexed scratch load)
+  const uint32_t b4 = (c & 16) ? ~0u : 0u, b3 = (c & 8) ? ~0u : 0u, b2 = (c & 4) ? ~0u : 0u,
+                 b1 = (c & 2) ? ~0u : 0u;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    p8[j] = sel_mask(b4, v[j + 8], v[j]) + __shfl_xor(sel_mask(b4, v[j], v[j + 8]), 16);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    p4[j] = sel_mask(b3, p8[j + 4], p8[j]) + __shfl_xor(sel_mask(b3, p8[j], p8[j + 4]), 8);
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    p2[j] = sel_mask(b2, p4[j + 2], p4[j]) + __shfl_xor(sel_mask(b2, p4[j], p4[j + 2]), 4);
+  const float p1 = sel_mask(b1, p2[1], p2[0]) + __shfl_xor(sel_mask(b1, p2[0], p2[1]), 2);
+  return p1 + __shfl_xor(p1, 1);
+}
+
+MLI_FI void field_points5(const float* center, const float* ray_unit, float d, int r, float e,
+                          float (&q)[TAPS][3]) {
+  const float px = __fadd_rn(center[3 * r + 0], __fmul_rn(ray_unit[3 * r + 0], d));
+  const float py = __fadd_rn(center[3 * r + 1], __fmul_rn(ray_unit[3 * r + 1], d));
+  const float pz = __fadd_rn(center[3 * r + 2], __fmul_rn(ray_unit[3 * r + 2], d));
+#pragma unroll
+  for (int pi = 0; pi < TAPS; ++pi) {
+    const float ex = (pi == 1 || pi == 4) ? e : -e;
+    const float ey = (pi == 3 || pi == 4) ? e : -e;
+    const float ez = (pi == 2 || pi == 4) ? e : -e;
+    q[pi][0] = pi ? __fadd_rn(px, ex) : px;
+    q[pi][1] = pi ? __fadd_rn(py, ey) : py;
+    q[pi][2] = pi ? __fadd_rn(pz, ez) : pz;
+  }
+}
+
+constexpr int LDS_SDFT_OFF = LDS_SDF;
+constexpr int LDS_DWS_OFF = LDS_SDF + MLI_SDF_T_PACK_BYTES;
+constexpr int LDS_SDF_BWD = LDS_DWS_OFF + 260 * 4;
+
+// Per sample: d sdf_i of the 5 points, then per point: layer 0 recomputed from the FIELD
+// encoding (as field_mlp_kernel), dZ0 = (w_sdf ds_i [+ W1^T dZ1 for the center]) *
+// softplus'(z0), d enc = W0_enc^T dZ0 (MFMA), dW/db of linear_sdf by lane reductions.
+__global__ __launch_bounds__(MLP_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_args a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  load_block(lds, a.wsdf, PIECES);
+  load_block(lds + LDS_SDFT_OFF, a.wsdf_t, SDFT_PIECES);
+  float* dws = reinterpret_cast<float*>(lds + LDS_DWS_OFF);
+  for (int i = threadIdx.x; i < 260; i += blockDim.x) dws[i] = 0.f;
+  vm_wait(0);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int S = a.R * a.N;
+  const int tiles = S / 32;
+  const float inv_scale = 1.0f / a.grad_scale;
+  const float inv_rn = 1.0f / (float)S;
+  for (int tile = blockIdx.x * MLP_WAVES + wave; tile < tiles; tile += gridDim.x * MLP_WAVES) {
+    const uint8_t* lds_t = lds + opaque_v(0);
+    const int m = tile * 32 + c;
+    const int r = m / a.N, k = m - r * a.N;
+    const size_t slot = (size_t)k * a.R + r;
+    float q[TAPS][3];
+    field_points5(a.center, a.ray_unit, a.dists[slot], r, a.eps, q);
+    // ---- d sdf of the 5 points (modules.py:157-175, model.py:343-347, misc.py:74-90)
+    const bool out = a.outside[r] != 0;
+    const float g0 = a.grad[3 * slot], g1 = a.grad[3 * slot + 1], g2 = a.grad[3 * slot + 2];
+    float dg0 = a.d_grad[3 * slot], dg1 = a.d_grad[3 * slot + 1], dg2 = a.d_grad[3 * slot + 2];
+    const float gn = sqrtf((g0 * g0 + g1 * g1) + g2 * g2);
+    if (!out && gn > 0.f) {  // eikonal: mean((|g| - 1)^2 * !outside)
+      const float e = (gn - 1.0f) * (gn - 1.0f);
+      if (isfinite(e)) {
+        const float f = a.w_eikonal * inv_rn * 2.0f * (gn - 1.0f) / gn;
+        dg0 += f * g0; dg1 += f * g1; dg2 += f * g2;
+      }
+    }
+    {  // F.normalize(g) backward, denominator max(|g|, 1e-12)
+      const float n0 = a.d_nrm[4 * slot] * inv_scale, n1 = a.d_nrm[4 * slot + 1] * inv_scale,
+                  n2 = a.d_nrm[4 * slot + 2] * inv_scale;
+      if (gn > 1e-12f) {
+        const float dot = (g0 * n0 + g1 * n1) + g2 * n2;
+        const float i1 = 1.0f / gn, i3 = dot / (gn * gn * gn);
+        dg0 += n0 * i1 - g0 * i3; dg1 += n1 * i1 - g1 * i3; dg2 += n2 * i1 - g2 * i3;
+      } else {
+        dg0 += n0 * 1e12f; dg1 += n1 * 1e12f; dg2 += n2 * 1e12f;
+      }
+    }
+    float dH = 0.f;  // d hxx: curvature mean(|sum(hess)| * !outside)
+    if (!out && a.hess) {
+      const float lap = (a.hess[3 * slot] + a.hess[3 * slot + 1]) + a.hess[3 * slot + 2];
+      if (isfinite(lap) && lap != 0.f) dH = a.w_curvature * inv_rn * (lap > 0.f ? 1.f : -1.f);
+    }
+    float ds[TAPS];
+    {
+      const float gd = 1.0f / a.grad_den, hh = 0.5f * dH / a.hess_den;
+      // grad = (k1 s1 + k2 s2 + k3 s3 + k4 s4) / (4 eps), k1=(1,-1,-1) k2=(-1,-1,1) k3=(-1,1,-1) k4=(1,1,1)
+      ds[1] = (dg0 - dg1 - dg2) * gd + hh;
+      ds[2] = (-dg0 - dg1 + dg2) * gd + hh;
+      ds[3] = (-dg0 + dg1 - dg2) * gd + hh;
+      ds[4] = (dg0 + dg1 + dg2) * gd + hh;
+      ds[0] = out ? 0.f : a.d_sdf[slot] - 2.0f * dH / a.hess_den;
+#pragma unroll
+      for (int i = 0; i < TAPS; ++i) ds[i] *= a.grad_scale;
+    }
+    if (h == 0) {  // db_sdf partial
+      float t = (((ds[0] + ds[1]) + ds[2]) + ds[3]) + ds[4];
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) t += __shfl_xor(t, o);
+      if (c == 0) atomicAdd(&dws[256], t);
+    }
+    const half8* encp = reinterpret_cast<const half8*>(a.enc + (size_t)tile * TAPS * 8 * 512) + opaque_v(lane);
+    const half8* dh0p = reinterpret_cast<const half8*>(a.dh0_frag + (size_t)tile * (16 * 64 * 8)) + lane;
+#pragma unroll 1
+    for (int pi = 0; pi < TAPS; ++pi) {
+      half8 E[8];
+#pragma unroll
+      for (int qq = 0; qq < 8; ++qq) E[qq] = encp[(pi * 8 + qq) * 64];
+      float px = q[0][0], py = q[0][1], pz = q[0][2], dsp = ds[0];
+#pragma unroll
+      for (int j = 1; j < TAPS; ++j) {
+        const uint32_t mk = pi == j ? ~0u : 0u;
+        px = sel_mask(mk, q[j][0], px);
+        py = sel_mask(mk, q[j][1], py);
+        pz = sel_mask(mk, q[j][2], pz);
+        dsp = sel_mask(mk, ds[j], dsp);
+      }
+      if (h == 0) {  // layer-0 input rows p (wgrad X rows 0..2), column pi*S + m
+        const size_t col = (size_t)pi * S + m, ld = (size_t)TAPS * S;
+        a.x0_rows[col] = __builtin_bit_cast(uint16_t, (f16)px);
+        a.x0_rows[ld + col] = __builtin_bit_cast(uint16_t, (f16)py);
+        a.x0_rows[2 * ld + col] = __builtin_bit_cast(uint16_t, (f16)pz);
+      }
+      // d enc = W0_enc^T dZ0 (4 n-tiles x 16 k-steps), accumulated as dZ0's k-steps 2t, 2t+1
+      // come out of tile t (no 16-fragment dZ0 array: it would need a runtime index)
+      f32x16 de[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) de[u][i] = 0.f;
+      half8* zdst = reinterpret_cast<half8*>(a.dz0_frag + ((size_t)pi * tiles + tile) * (16 * 64 * 8)) + lane;
+#pragma unroll 1
+      for (int t = 0; t < 8; ++t) {
+        const uint8_t* lt = lds + opaque_v(0);
+        float b0[16], wx[16], wy[16], wz[16], ws[16];
+        load_rowc(lt, 0, t, h, b0);
+        load_rowc(lt, 1, t, h, wx);
+        load_rowc(lt, 2, t, h, wy);
+        load_rowc(lt, 3, t, h, wz);
+        f32x16 acc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = b0[i] + (wx[i] * px + wy[i] * py + wz[i] * pz);
+        const half8* frag = reinterpret_cast<const half8*>(lt + t * 8 * 1024) + lane;
+#pragma unroll
+        for (int qq = 0; qq < 8; ++qq) acc = mfma32(frag[qq * 64], E[qq], acc);
+        load_rowc(lt, 4, t, h, ws);
+        half8 c0, c1;
+        if (pi == 0) { c0 = dh0p[(2 * t) * 64]; c1 = dh0p[(2 * t + 1) * 64]; }
+        f32x16 dz;
+        float part[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          // torch softplus backward: z = e^{beta x}; beta x > 20 ? 1 : z / (z + 1)
+          const float tt = acc[i] * 100.0f;
+          const float e = __builtin_amdgcn_exp2f(tt * 1.4426950408889634f);
+          const float dsig = tt > 20.0f ? 1.0f : e / (e + 1.0f);
+          float dh = ws[i] * dsp;
+          if (pi == 0) dh += (float)((i < 8) ? c0[i] : c1[i - 8]);
+          dz[i] = dh * dsig;
+          part[i] = dsp * softplus100(acc[i]);
+        }
+        const half8 z0 = acc_to_frag(dz, 0), z1 = acc_to_frag(dz, 1);
+        __builtin_nontemporal_store(z0, zdst + (2 * t) * 64);
+        __builtin_nontemporal_store(z1, zdst + (2 * t + 1) * 64);
+        const half8* fr = reinterpret_cast<const half8*>(lt + LDS_SDFT_OFF + (2 * t) * 1024) + lane;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          de[u] = mfma32(fr[(u * 16) * 64], z0, de[u]);
+          de[u] = mfma32(fr[(u * 16 + 1) * 64], z1, de[u]);
+        }
+        const float tot = half_reduce16(part, c);
+        if ((c & 1) == 0) atomicAdd(&dws[32 * t + acc_row((c >> 1) & 15, h)], tot);
+      }
+      float* dst = a.d_enc + ((size_t)(tile * TAPS + pi) * 8) * 512 + lane * 8;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          f32x4* o = reinterpret_cast<f32x4*>(dst + (size_t)(2 * u + s2) * 512);
+          const f32x16& v = de[u];
+          __builtin_nontemporal_store(f32x4{v[8 * s2] * inv_scale, v[8 * s2 + 1] * inv_scale,
+                                            v[8 * s2 + 2] * inv_scale, v[8 * s2 + 3] * inv_scale}, o);
+          __builtin_nontemporal_store(f32x4{v[8 * s2 + 4] * inv_scale, v[8 * s2 + 5] * inv_scale,
+                                            v[8 * s2 + 6] * inv_scale, v[8 * s2 + 7] * inv_scale}, o + 1);
+        }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 257; i += blockDim.x) {
+    const float v = dws[i];
+    if (v != 0.f) unsafeAtomicAdd(i < 256 ? a.dw_sdf + i : a.db_sdf, v);
+  }
+}
+
+// Hash-grid backward, level-outer like encode5_kernel: lane (c, h) = sample c, level 2qq+h.
+// The center's 8 corners take the weighted d enc of every point in the center's cell (one
+// fp32 atomic per corner feature); a tap in another cell scatters its own 64.
+__global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int S = a.R * a.N;
+  const int tile = blockIdx.x * 4 + wave;
+  if (tile >= S / 32) return;
+  const int m = tile * 32 + c;
+  const int r = m / a.N, k = m - r * a.N;
+  float q[TAPS][3];
+  field_points5(a.center, a.ray_unit, a.dists[(size_t)k * a.R + r], r, a.eps, q);
+  float x[TAPS][3];
+#pragma unroll
+  for (int p = 0; p < TAPS; ++p)
+#pragma unroll
+    for (int d = 0; d < 3; ++d) x[p][d] = (q[p][d] + 2.0f) * 0.25f;
+  const float* src = a.d_enc + ((size_t)tile * TAPS * 8) * 512 + lane * 8;
+#pragma unroll 1
+  for (int qq = 0; qq < 8; ++qq) {
+    if (2 * qq >= a.active_levels) break;
+    const int lv = 2 * qq + h;
+    if (lv >= a.active_levels) continue;
+    const LevelP P = level_params(a.levels, lv);
+    const bool dense = level_dense(a.levels, lv);
+    const uint32_t r2 = P.res * P.res;
+    auto index_of = [&](uint32_t cx, uint32_t cy, uint32_t cz) MLI_LAMBDA_FI {
+      return dense ? fastmod_u32(cx + cy * P.res + cz * r2, P.magic, P.size)
+                   : ((cx ^ (cy * 2654435761u) ^ (cz * 805459861u)) & (P.size - 1u));
+    };
+    auto cell = [&](const float (&xp)[3], uint32_t (&g)[3], float (&pos)[3]) MLI_LAMBDA_FI {
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const float p = fmaf(P.scale, xp[d], 0.5f);
+        const float fl = floorf(p);
+        g[d] = (uint32_t)(int)fl;
+        pos[d] = p - fl;
+      }
+    };
+    auto weight = [&](const float (&pos)[3], int cc) MLI_LAMBDA_FI {
+      float w = 1.0f;
+      w *= (cc & 1) ? pos[0] : 1.0f - pos[0];
+      w *= ((cc >> 1) & 1) ? pos[1] : 1.0f - pos[1];
+      w *= ((cc >> 2) & 1) ? pos[2] : 1.0f - pos[2];
+      return w;
+    };
+    auto scatter = [&](const uint32_t (&g)[3], const float (&G)[8][8]) MLI_LAMBDA_FI {
+#pragma unroll
+      for (int cc = 0; cc < 8; ++cc) {
+        const uint32_t idx = index_of(g[0] + (cc & 1), g[1] + ((cc >> 1) & 1), g[2] + ((cc >> 2) & 1));
+        float* dstp = a.d_table + (size_t)(P.offset + idx) * 8;
+#pragma unroll
+        for (int f = 0; f < 8; ++f) unsafeAtomicAdd(dstp + f, G[cc][f]);
+      }
+    };
+    uint32_t g0[3];
+    float pos0[3];
+    cell(x[0], g0, pos0);
+    float G[8][8];
+    {
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(src + (size_t)qq * 512);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(src + (size_t)qq * 512 + 4);
+      const float d[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+      for (int cc = 0; cc < 8; ++cc) {
+        const float w = weight(pos0, cc);
+#pragma unroll
+        for (int f = 0; f < 8; ++f) G[cc][f] = w * d[f];
+      }
+    }
+#pragma unroll 1
+    for (int p = 1; p < TAPS; ++p) {
+      const float* sp = src + ((size_t)p * 8 + qq) * 512;
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(sp);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(sp + 4);
+      const float d[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      float xp[3] = {x[0][0], x[0][1], x[0][2]};
+#pragma unroll
+      for (int j = 1; j < TAPS; ++j) {
+        const uint32_t mk = p == j ? ~0u : 0u;
+        xp[0] = sel_mask(mk, x[j][0], xp[0]);
+        xp[1] = sel_mask(mk, x[j][1], xp[1]);
+        xp[2] = sel_mask(mk, x[j][2], xp[2]);
+      }
+      uint32_t g[3];
+      float pos[3];
+      cell(xp, g, pos);
+      if (g[0] == g0[0] && g[1] == g0[1] && g[2] == g0[2]) {
+#pragma unroll
+        for (int cc = 0; cc < 8; ++cc) {
+          const float w = weight(pos, cc);
+#pragma unroll
+          for (int f = 0; f < 8; ++f) G[cc][f] = fmaf(w, d[f], G[cc][f]);
+        }
+      } else {
+        float T[8][8];
+#pragma unroll
+        for (int cc = 0; cc < 8; ++cc) {
+          const float w = weight(pos, cc);
+#pragma unroll
+          for (int f = 0; f < 8; ++f) T[cc][f] = w * d[f];
+        }
+        scatter(g, T);
+      }
+    }
+    scatter(g0, G);
+  }
+}
+
 }  // namespace
 
 extern "C" int mli_sdf(const mli_sdf_args* a, mli_stream_t s) {
@@ -446,5 +806,30 @@ extern "C" int mli_hashgrid_fwd(const mli_hashgrid_args* a, mli_stream_t s) {
 
 extern "C" int mli_pack_sdf(const mli_pack_sdf_args* a, mli_stream_t s) {
   hipLaunchKernelGGL(pack_sdf_kernel, dim3(256), dim3(256), 0, (hipStream_t)s, *a);
+  MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_pack_sdf_t(const mli_pack_sdf_t_args* a, mli_stream_t s) {
+  hipLaunchKernelGGL(pack_sdf_t_kernel, dim3(64), dim3(256), 0, (hipStream_t)s, *a);
+  MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_sdf_bwd(const mli_sdf_bwd_args* a, mli_stream_t s) {
+  const int S = a->R * a->N;
+  if (S <= 0) return 0;
+  if (S % 256 != 0 || !a->enc || !a->wsdf || !a->wsdf_t || !a->d_enc || !a->dz0_frag || !a->x0_rows ||
+      !a->dw_sdf || !a->db_sdf || !a->dh0_frag || !a->d_nrm || !a->d_sdf || !a->d_grad)
+    return (int)hipErrorInvalidValue;
+  int blocks = S / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(sdf_bwd_kernel, dim3(blocks), dim3(MLP_WAVES * 64), LDS_SDF_BWD, (hipStream_t)s, *a);
+  MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_hash_bwd(const mli_hash_bwd_args* a, mli_stream_t s) {
+  const int S = a->R * a->N;
+  if (S <= 0) return 0;
+  if (S % 32 != 0 || !a->d_enc || !a->d_table) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(hash_bwd_kernel, dim3((S / 32 + 3) / 4), dim3(256), 0, (hipStream_t)s, *a);
   MLI_LAUNCH_CHECK();
 }

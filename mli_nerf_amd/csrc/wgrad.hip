@@ -148,6 +148,35 @@ __global__ __launch_bounds__(512) void wgrad_kernel(KArgs ka) {
   }
 }
 
+
+// Frag image -> feature-major rows (the wgrad operand layout), 8 tiles = 256 samples per
+// workgroup, one k-step at a time through an LDS transpose so every row leaves as 512 B.
+constexpr int FR_ROW = 256 * 2 + 16;
+__global__ __launch_bounds__(512) void frag_rows_kernel(mli_frag_rows_args a) {
+  __shared__ __attribute__((aligned(16))) uint8_t st[16 * FR_ROW];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+  const int c = lane & 31, h = lane >> 5;
+  const int tile = blockIdx.x * 8 + wave;
+  const bool have = tile < a.tiles;
+  const half8* src = reinterpret_cast<const half8*>(a.src + (size_t)(have ? tile : 0) * a.tile_stride) + lane;
+  for (int q = 0; q < a.k_steps; ++q) {
+    half8 v = src[q * 64];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kk = a.order ? (8 * (j >> 2) + 4 * h + (j & 3)) : (8 * h + j);
+      *reinterpret_cast<f16*>(st + kk * FR_ROW + (wave * 32 + c) * 2) = v[j];
+    }
+    __syncthreads();
+    const int row = tid >> 5, col = (tid & 31) * 8;
+    const int64_t s0 = (int64_t)blockIdx.x * 256 + col;
+    if (s0 < (int64_t)a.tiles * 32) {
+      const u32x4 x = *reinterpret_cast<const u32x4*>(st + row * FR_ROW + col * 2);
+      __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(a.dst + (a.row0 + 16 * q + row) * a.ld + a.col0 + s0));
+    }
+    __syncthreads();
+  }
+}
+
 enum { CLS_BIG = 1, CLS_WIDE = 2, CLS_THIN = 4 };
 
 inline int job_class(const mli_wgrad_job& j) {
@@ -194,4 +223,11 @@ extern "C" int mli_wgrad(const mli_wgrad_args* a, mli_stream_t s) {
   if (!e && (a->classes & CLS_WIDE)) e = launch<256, 320, 4, 2, 1, 1>(a, CLS_WIDE, (hipStream_t)s);
   if (!e && (a->classes & CLS_THIN)) e = launch<32, 256, 1, 8, 2, 2>(a, CLS_THIN, (hipStream_t)s);
   return e;
+}
+
+extern "C" int mli_frag_rows(const mli_frag_rows_args* a, mli_stream_t s) {
+  if (a->tiles <= 0 || a->k_steps <= 0) return 0;
+  if (a->tiles % 8 != 0 || (a->ld % 8) != 0 || (a->col0 % 8) != 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(frag_rows_kernel, dim3(a->tiles / 8), dim3(512), 0, (hipStream_t)s, *a);
+  MLI_LAUNCH_CHECK();
 }

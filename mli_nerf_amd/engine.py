@@ -54,23 +54,26 @@ def _to_device_structs(structs, device):
 
 
 class RenderEngine:
-    def __init__(self, cfg, device):
+    """``stage`` 'b': LumenRGB 'rgb_r_s' (three heads, frozen geometry); 'a': mode 'rgb' (one
+    head) with the geometry trained -- hash table, SDF MLP and s_var (backward_a)."""
+
+    def __init__(self, cfg, device, stage="b"):
         self.cfg = cfg
+        self.stage = stage
+        self.head_specs = layout.HEADS_A if stage == "a" else layout.HEADS
         self.device = torch.device(device)
         self.levels, self.table_entries = _grid_levels(cfg)
-        eps64 = normal_eps(cfg.levels, cfg.min_logres, cfg.max_logres) / np.sqrt(3)
-        self.eps = float(np.float32(eps64))
-        self.grad_den = float(np.float32(4.0 * eps64))
-        self.hess_den = float(np.float32(eps64 ** 2))
+        self.set_normal_eps(normal_eps(cfg.levels, cfg.min_logres, cfg.max_logres))
+        self.active_levels = cfg.levels
         self.table16 = None
-        self.wsdf = torch.empty(C.sizeof(C.c_uint8) * (65536 + 5 * 1024 + 16), dtype=torch.uint8,
-                                device=self.device)
-        self.fplan, fbytes = layout.fwd_plan()
-        self.bplan, bbytes = layout.bwd_plan()
+        self.wsdf = torch.empty(65536 + 5 * 1024 + 16, dtype=torch.uint8, device=self.device)
+        self.fplan, fbytes = layout.fwd_plan(self.head_specs)
+        self.bplan, bbytes = layout.geo_plan() if stage == "a" else layout.bwd_plan()
         self.wfwd = torch.empty(fbytes, dtype=torch.uint8, device=self.device)
         self.wbwd = torch.empty(bbytes, dtype=torch.uint8, device=self.device)
+        self.wsdf_t = torch.empty(65536, dtype=torch.uint8, device=self.device) if stage == "a" else None
         self._kmaps = []  # keep host kmap tensors alive
-        self.tlayout, self.n_train = layout.trainable_layout()
+        self.tlayout, self.n_train = layout.trainable_layout(stage)
         self.toff = {name: (off, shape) for name, shape, off in self.tlayout}
         self._bufs = {}
         self.u_fine = (C.c_float * 64)(*(layout.u_fine(cfg.n_fine) + [2.0] * (64 - cfg.n_fine)))
@@ -78,34 +81,57 @@ class RenderEngine:
         self.trace = None  # set to a list to record per-round sampler outputs (debug/tests)
 
     # ------------------------------------------------------------------ parameters
-    def load_sdf(self, params_flat, v0, g0, b0, w_sdf, b_sdf):
-        """Frozen geometry (stage b): fp16 shadow of the hash table + packed layer 0."""
+    def set_normal_eps(self, normal_eps_value):
+        """Tap epsilon normal_eps / sqrt(3) (modules.py:102-107,159) and the fp32 denominators
+        of the gradient / hessian stencils (:167,172)."""
+        eps64 = float(normal_eps_value) / np.sqrt(3)
+        self.eps = float(np.float32(eps64))
+        self.grad_den = float(np.float32(4.0 * eps64))
+        self.hess_den = float(np.float32(eps64 ** 2))
+
+    def load_table(self, params_flat):
+        """fp16 gather shadow of the hash table (tcnn precision)."""
         assert params_flat.numel() == self.table_entries * 8, (params_flat.numel(), self.table_entries)
-        self.table16 = torch.empty(params_flat.numel(), dtype=torch.float16, device=self.device)
+        if self.table16 is None or self.table16.numel() != params_flat.numel():
+            self.table16 = torch.empty(params_flat.numel(), dtype=torch.float16, device=self.device)
         L.call("mli_cast_f16", L.CastArgs(L.ptr(params_flat), L.ptr(self.table16), params_flat.numel()))
+
+    def pack_sdf(self, v0, g0, b0, w_sdf, b_sdf):
+        """SDF layer 0 + sdf head block (and, in stage a, W0_enc^T for the backward)."""
         L.call("mli_pack_sdf", L.PackSdfArgs(L.ptr(v0), L.ptr(g0), L.ptr(b0), L.ptr(w_sdf), L.ptr(b_sdf),
                                              L.ptr(self.wsdf)))
+        if self.wsdf_t is not None:
+            L.call("mli_pack_sdf_t", L.PackSdfTArgs(L.ptr(v0), L.ptr(g0), L.ptr(self.wsdf_t)))
+
+    def load_sdf(self, params_flat, v0, g0, b0, w_sdf, b_sdf):
+        """Frozen geometry (stage b): fp16 shadow of the hash table + packed layer 0."""
+        self.load_table(params_flat)
+        self.pack_sdf(v0, g0, b0, w_sdf, b_sdf)
 
     def _descs(self, plan, tensors):
         descs = []
         for p in plan:
             km = torch.from_numpy(p["kmap"].astype(np.int16)).to(self.device)
             kmode = torch.from_numpy(p["kmode"].astype(np.uint8)).to(self.device)
-            self._kmaps += [km, kmode]
+            nm = None
+            if p.get("nmap") is not None:
+                nm = torch.from_numpy(p["nmap"].astype(np.int16)).to(self.device)
+            self._kmaps += [km, kmode, nm]
             v, g, b = tensors(p["prefix"])
             descs.append(L.PackLayer(L.ptr(v), L.ptr(g), L.ptr(b), p["n_out"], p["k_ref"], p["transpose"],
                                      p["n_tiles"], p["k_steps"], L.ptr(km), L.ptr(kmode), p["dst_offset"],
-                                     p["chunk_stride"]))
+                                     p["chunk_stride"], L.ptr(nm)))
         return descs
 
     def pack_heads(self, flat, sdf_l1):
-        """Weight-norm fold + fp16 fragment packing of SDF layer 1 and the three heads
-        (forward image) and of the transposed head layers (backward image)."""
+        """Weight-norm fold + fp16 fragment packing of SDF layer 1 and the heads (forward
+        image) and of the transposed layers of the backward (stage b: the heads' dX chain;
+        stage a: the geometry chain, layout.geo_plan)."""
         def tensors(prefix):
-            if prefix == "neural_sdf.mlp.linears.1":
+            if prefix == "neural_sdf.mlp.linears.1" and sdf_l1 is not None:
                 return sdf_l1
             return tuple(self.param_view(flat, prefix + s) for s in (".weight_v", ".weight_g", ".bias"))
-        key = (flat.data_ptr(), sdf_l1[0].data_ptr())
+        key = (flat.data_ptr(), None if sdf_l1 is None else sdf_l1[0].data_ptr())
         if self._pack_descs is None or self._pack_descs[0] != key:
             self._kmaps = []
             fd = _to_device_structs(self._descs(self.fplan, tensors), self.device)
@@ -120,7 +146,7 @@ class RenderEngine:
     def param_view(self, flat, name):
         off, shape = self.toff[name]
         n = int(np.prod(shape))
-        return flat[off:off + n].view(*shape)
+        return flat[off:off + n].reshape(shape)
 
     # ------------------------------------------------------------------ buffers
     def _buf(self, name, shape, dtype=torch.float32):
@@ -161,7 +187,7 @@ class RenderEngine:
                                     L.ptr(dists), L.ptr(rays["outside"]), L.ptr(self.table16), self.levels,
                                     L.ptr(self.wsdf), self.eps, self.grad_den, self.hess_den,
                                     self.cfg.outside_val, 1 if hess is not None else 0, L.ptr(out),
-                                    L.ptr(grad), L.ptr(hess), L.ptr(h0), L.ptr(enc)))
+                                    L.ptr(grad), L.ptr(hess), L.ptr(h0), L.ptr(enc), int(self.active_levels)))
 
     @torch.no_grad()
     def sample(self, rays, u=None):
@@ -208,24 +234,27 @@ class RenderEngine:
         hess = self._buf("hess", (N, R, 3)) if training else None
         h0 = self._buf("h0", (S * 256,), torch.float16)
         self._sdf(rays, dists, N, sdf, mode=1, grad=grad, hess=hess, h0=h0)
-        return dict(sdf=sdf, grad=grad, hess=hess, h0=h0)
+        return dict(sdf=sdf, grad=grad, hess=hess, h0=h0, enc=self._bufs["enc5"])
 
     @torch.no_grad()
     def heads(self, rays, dists, fld, training):
         N, R = dists.shape
         S = N * R
+        nh = len(self.head_specs)
         y = self._buf("y", (N, R, 8))
+        if nh == 1:
+            y.zero_()  # o_r / o_s slots the single head does not write (composite reads them)
         feat = self._buf("feat", (S * 256,), torch.float16)
         x0T = xT = masks = None
         if training:
             x0T = self._buf("x0T", (layout.K0, S), torch.float16)
-            xT = self._buf("xT", (3, 4, 256, S), torch.float16)
-            masks = self._buf("masks", (3, 4, S // 32, 64, 4), torch.int32)
+            xT = self._buf("xT", (nh, 4, 256, S), torch.float16)
+            masks = self._buf("masks", (nh, 4, S // 32, 64, 4), torch.int32)
         L.call("mli_rgb_fwd", L.RgbFwdArgs(R, N, L.ptr(rays["center"]), L.ptr(rays["ray_unit"]),
                                            L.ptr(rays["pts_light"]), L.ptr(dists), L.ptr(fld["grad"]),
                                            L.ptr(fld["h0"]), L.ptr(self.wfwd), L.ptr(y), L.ptr(feat),
-                                           L.ptr(x0T), L.ptr(xT), L.ptr(masks)))
-        return dict(y=y, x0T=x0T, xT=xT, masks=masks)
+                                           L.ptr(x0T), L.ptr(xT), L.ptr(masks), nh))
+        return dict(y=y, x0T=x0T, xT=xT, masks=masks, feat=feat)
 
     @torch.no_grad()
     def composite(self, rays, dists, fld, hd, s_var, progress, training):
@@ -329,3 +358,126 @@ class RenderEngine:
         L.call("mli_grad_assemble", L.AssembleArgs(15, L.ptr(ad), 1.0 / scale))
         return grad_out
 
+
+    # ------------------------------------------------------------------ stage a backward
+    def _assemble_desc(self, dw, db, v, g, n_out, k_ref, k_pack, kinv, gv, gg, gb, plain=0):
+        kinv_t = torch.from_numpy(np.asarray(kinv).astype(np.int16)).to(self.device)
+        return L.AssembleLayer(L.ptr(dw), L.ptr(db), L.ptr(v), L.ptr(g), n_out, k_ref, k_pack, L.ptr(kinv_t),
+                               L.ptr(gv), L.ptr(gg), L.ptr(gb), None, plain), kinv_t
+
+    def _plan_a(self, bufs, flat, grad_flat, S):
+        """wgrad jobs (two launches: S samples, 5S samples) + assemble descriptors, cached."""
+        key = tuple(t.data_ptr() for t in bufs.values()) + (flat.data_ptr(), grad_flat.data_ptr(), S)
+        if getattr(self, "_aplan", None) is not None and self._aplan[0] == key:
+            return self._aplan[1:]
+        head = layout.HEADS_A[0][0]
+        sizes = [(256, layout.K0), (256, 256), (256, 256), (256, 256), (3, 256)]
+        dw, off = bufs["dw"], 0
+        jobs_s, jobs_5s, descs, keep = [], [], [], []
+
+        def take(m, k):
+            nonlocal off
+            w, b = dw[off:off + m * k], dw[off + m * k:off + m * k + m]
+            off += m * k + m
+            return w, b
+        pv = lambda n: self.param_view(flat, n)  # noqa: E731
+        gv = lambda n: self.param_view(grad_flat, n)  # noqa: E731
+        for li, (m, k) in enumerate(sizes):
+            w, b = take(m, k)
+            a_rows = bufs["dzT"][li] if li < 4 else bufs["dz4T"]
+            b_rows = bufs["x0T"] if li == 0 else bufs["xT"][0, li - 1]
+            jobs_s.append(L.WgradJob(L.ptr(a_rows), L.ptr(b_rows), m, k, L.ptr(w), L.ptr(b), k))
+            pre = layout.param_prefix(head, li)
+            k_ref = pv(pre + ".weight_v").shape[1]
+            kinv = layout.head_kinv(head, k_ref) if li == 0 else np.arange(k_ref)
+            d, kt = self._assemble_desc(w, b, pv(pre + ".weight_v"), pv(pre + ".weight_g"), m, k_ref, k, kinv,
+                                        gv(pre + ".weight_v"), gv(pre + ".weight_g"), gv(pre + ".bias"))
+            descs.append(d)
+            keep.append(kt)
+        # neural_sdf.mlp.linears.1: dZ1sdf x h0 (S samples)
+        w, b = take(256, 256)
+        jobs_s.append(L.WgradJob(L.ptr(bufs["dz1T"]), L.ptr(bufs["h0_rows"]), 256, 256, L.ptr(w), L.ptr(b), 256))
+        pre = "neural_sdf.mlp.linears.1"
+        d, kt = self._assemble_desc(w, b, pv(pre + ".weight_v"), pv(pre + ".weight_g"), 256, 256, 256,
+                                    np.arange(256), gv(pre + ".weight_v"), gv(pre + ".weight_g"), gv(pre + ".bias"))
+        descs.append(d)
+        keep.append(kt)
+        # neural_sdf.mlp.linears.0: dZ0 x [p, enc] of the 5 points (5S samples)
+        w, b = take(256, layout.SDF_K0)
+        jobs_5s.append(L.WgradJob(L.ptr(bufs["dz0_rows"]), L.ptr(bufs["x0_rows"]), 256, layout.SDF_K0, L.ptr(w),
+                                  L.ptr(b), layout.SDF_K0))
+        pre = "neural_sdf.mlp.linears.0"
+        d, kt = self._assemble_desc(w, b, pv(pre + ".weight_v"), pv(pre + ".weight_g"), 256, layout.SDF_K0,
+                                    layout.SDF_K0, np.arange(layout.SDF_K0), gv(pre + ".weight_v"),
+                                    gv(pre + ".weight_g"), gv(pre + ".bias"))
+        descs.append(d)
+        keep.append(kt)
+        # linear_sdf (plain Linear): in-kernel reductions of mli_sdf_bwd
+        dws = bufs["dws"]
+        d, kt = self._assemble_desc(dws[:256], dws[256:257], None, None, 1, 256, 256, np.arange(256),
+                                    gv("neural_sdf.mlp.linear_sdf.weight"), None,
+                                    gv("neural_sdf.mlp.linear_sdf.bias"), plain=1)
+        descs.append(d)
+        keep.append(kt)
+        js = (L.WgradJob * len(jobs_s))(*jobs_s)
+        j5 = (L.WgradJob * len(jobs_5s))(*jobs_5s)
+        ad = _to_device_structs(descs, self.device)
+        self._aplan = (key, js, j5, ad, len(descs), keep, off)
+        return self._aplan[1:]
+
+    @torch.no_grad()
+    def backward_a(self, st, d_rgb, flat, grad_flat, grad_table, w_eikonal, w_curvature, progress):
+        """Stage-a gradient of the loss w.r.t. every parameter: the flat buffer (SDF MLP, head,
+        s_var) into grad_flat and the hash table into grad_table (both fully overwritten)."""
+        rays, dists, fld, hd, comp = st
+        N, R = dists.shape
+        S = N * R
+        T = S // 32
+        scale = float(2.0 ** round(math.log2(max(R, 1)) + 2))
+        f16 = torch.float16
+        dz4, d_sdf, d_grad = self._buf("dz4", (N, R, 8)), self._buf("d_sdf", (N, R)), self._buf("d_grad", (N, R, 3))
+        dinv = self._buf("d_inv_s", (1,))
+        dinv.zero_()
+        anneal = min(progress / self.cfg.anneal_end, 1.0)
+        s_var = self.param_view(flat, "s_var")
+        L.call("mli_composite_bwd_geo", L.CompositeBwdGeoArgs(
+            R, N, L.ptr(dists), L.ptr(rays["far"]), L.ptr(rays["ray_unit"]), L.ptr(fld["sdf"]), L.ptr(fld["grad"]),
+            L.ptr(hd["y"]), L.ptr(s_var), float(anneal), 1 if self.cfg.white_bg else 0, L.ptr(d_rgb.contiguous()),
+            scale, L.ptr(dz4), L.ptr(d_sdf), L.ptr(d_grad), L.ptr(dinv), L.ptr(self.param_view(grad_flat, "s_var"))))
+        b = dict(dzT=self._buf("dzT", (4, 256, S), f16), dz4T=self._buf("dz4T", (4, S), f16),
+                 x0T=hd["x0T"], xT=hd["xT"], dz1T=self._buf("dz1T", (256, S), f16),
+                 h0_rows=self._buf("h0_rows", (256, S), f16), dz0_rows=self._buf("dz0_rows", (256, 5 * S), f16),
+                 x0_rows=self._buf("x0_rows", (layout.SDF_K0, 5 * S), f16), dws=self._buf("dws", (257,)))
+        d_nrm = self._buf("d_nrm", (N, R, 4))
+        dh0 = self._buf("dh0", (S * 256,), f16)
+        L.call("mli_geo_bwd", L.GeoBwdArgs(R, N, L.ptr(dz4), L.ptr(self.wbwd), L.ptr(hd["masks"]), L.ptr(hd["feat"]),
+                                           L.ptr(b["dzT"]), L.ptr(b["dz4T"]), L.ptr(d_nrm), L.ptr(b["dz1T"]),
+                                           L.ptr(dh0)))
+        d_enc = self._buf("d_enc", (S * 640,))
+        dz0f = self._buf("dz0_frag", (5 * S * 256,), f16)
+        b["dws"].zero_()
+        L.call("mli_sdf_bwd", L.SdfBwdArgs(
+            R, N, L.ptr(rays["center"]), L.ptr(rays["ray_unit"]), L.ptr(dists), L.ptr(rays["outside"]),
+            L.ptr(fld["grad"]), L.ptr(fld["hess"]), L.ptr(d_sdf), L.ptr(d_grad), L.ptr(d_nrm), L.ptr(dh0),
+            L.ptr(fld["enc"]), L.ptr(self.wsdf), L.ptr(self.wsdf_t), self.eps, self.grad_den, self.hess_den,
+            float(w_eikonal), float(w_curvature), scale, L.ptr(d_enc), L.ptr(dz0f), L.ptr(b["x0_rows"]),
+            L.ptr(b["dws"][:256]), L.ptr(b["dws"][256:])))
+        grad_table.zero_()
+        L.call("mli_hash_bwd", L.HashBwdArgs(R, N, L.ptr(rays["center"]), L.ptr(rays["ray_unit"]), L.ptr(dists),
+                                             L.ptr(d_enc), self.levels, self.eps, int(self.active_levels),
+                                             L.ptr(grad_table)))
+        # feature-major operand rows of the SDF weight gradients
+        L.call("mli_frag_rows", L.FragRowsArgs(L.ptr(fld["h0"]), 16 * 512, T, 16, 1, L.ptr(b["h0_rows"]), S, 0, 0))
+        for pi in range(5):
+            L.call("mli_frag_rows", L.FragRowsArgs(L.ptr(fld["enc"]) + pi * 8 * 512 * 2, 5 * 8 * 512, T, 8, 0,
+                                                   L.ptr(b["x0_rows"]), 5 * S, pi * S, 3))
+        L.call("mli_frag_rows", L.FragRowsArgs(L.ptr(dz0f), 16 * 512, 5 * T, 16, 1, L.ptr(b["dz0_rows"]), 5 * S, 0, 0))
+        dw_total = sum(m * k + m for m, k in [(256, layout.K0), (256, 256), (256, 256), (256, 256), (3, 256),
+                                              (256, 256), (256, layout.SDF_K0)])
+        b["dw"] = self._buf("dw_a", (dw_total,))
+        js, j5, ad, n_desc, _, _ = self._plan_a(b, flat, grad_flat, S)
+        b["dw"].zero_()
+        L.call("mli_wgrad", L.WgradArgs(S, len(js), C.cast(js, C.c_void_p), 7))
+        L.call("mli_wgrad", L.WgradArgs(5 * S, len(j5), C.cast(j5, C.c_void_p), 7))
+        L.call("mli_grad_assemble", L.AssembleArgs(n_desc, L.ptr(ad), 1.0 / scale))
+        return grad_flat, grad_table

@@ -13,6 +13,8 @@ Reference column order of each head's first Linear (NeuralLumen/utils/modules.py
 import numpy as np
 
 HEADS = (("mlp", 294, 3), ("mlp_r", 262, 3), ("mlp_s", 278, 1))
+HEADS_A = HEADS[:1]   # LumenRGB mode 'rgb' (stage a): the single 294 -> 3 head, input order as 'mlp'
+SDF_K0 = 131          # neural_sdf.mlp.linears.0 input: p 3 + hash encoding 128
 HIDDEN = 256
 K0 = 304
 KS0 = 19
@@ -59,11 +61,22 @@ def param_prefix(head, layer):
     return "neural_rgb.%s.linears.%d" % (head, layer)
 
 
-def trainable_layout():
-    """Flat fp32 buffer layout of the stage-b trainable parameters (partial_grad neural_rgb,
-    NeuralLumen/trainer.py:44-54): [(name, shape, offset)]."""
+def trainable_layout(stage="b"):
+    """Flat fp32 buffer layout of the trainable parameters: [(name, shape, offset)].
+    Stage b (partial_grad neural_rgb, NeuralLumen/trainer.py:44-54): the three heads.
+    Stage a (every parameter, NeuralLumen/model.py:422-438): the SDF MLP, the single head and
+    s_var -- the hash table is a separate buffer (``neural_sdf.tcnn_encoding.params``)."""
     out, off = [], 0
-    for head, k_in, k_out in HEADS:
+    if stage == "a":
+        for li, k_in in enumerate((SDF_K0, HIDDEN)):
+            pre = "neural_sdf.mlp.linears.%d" % li
+            for suffix, shape in (("weight_v", (HIDDEN, k_in)), ("weight_g", (HIDDEN, 1)), ("bias", (HIDDEN,))):
+                out.append((pre + "." + suffix, shape, off))
+                off += int(np.prod(shape))
+        for suffix, shape in (("weight", (1, HIDDEN)), ("bias", (1,))):
+            out.append(("neural_sdf.mlp.linear_sdf." + suffix, shape, off))
+            off += int(np.prod(shape))
+    for head, k_in, k_out in (HEADS_A if stage == "a" else HEADS):
         dims = [k_in] + [HIDDEN] * 4 + [k_out]
         for li in range(5):
             pre = param_prefix(head, li)
@@ -71,15 +84,18 @@ def trainable_layout():
                                   ("bias", (dims[li + 1],))):
                 out.append((pre + "." + suffix, shape, off))
                 off += int(np.prod(shape))
+    if stage == "a":
+        out.append(("s_var", (), off))
+        off += 1
     return out, off
 
 
-def fwd_plan():
+def fwd_plan(heads=HEADS):
     """Chunk sequence of the forward weight image, in kernel consumption order.
     Each entry: dict(param prefix, n_out, k_ref, transpose, n_tiles, k_steps, kmap, kmode)."""
     plan = [dict(prefix="neural_sdf.mlp.linears.1", n_out=256, k_ref=256, transpose=0, n_tiles=8,
                  k_steps=16, kmap=ident_kmap(256, 256), kmode=np.full(16, ACC, np.uint8))]
-    for head, k_in, k_out in HEADS:
+    for head, k_in, k_out in heads:
         kmode0 = np.array([ACC] * 16 + [NAT] * 3, np.uint8)
         plan.append(dict(prefix=param_prefix(head, 0), n_out=256, k_ref=k_in, transpose=0, n_tiles=8,
                          k_steps=KS0, kmap=head_kmap(head), kmode=kmode0))
@@ -103,6 +119,24 @@ def bwd_plan():
             plan.append(dict(prefix=param_prefix(head, li), n_out=256, k_ref=256, transpose=1,
                              n_tiles=8, k_steps=16, kmap=ident_kmap(256, 256),
                              kmode=np.full(16, ACC, np.uint8)))
+    return _with_offsets(plan)
+
+
+def geo_plan():
+    """Stage-a backward image (mli_geo_bwd): the single head's W4^T, W3^T, W2^T, W1^T, then
+    W0^T over the packed input rows 0..287 (feat in ACC order, p, normal; row map = head_kmap),
+    then SDF layer 1 transposed (rows = h0 index, k = its outputs in ACC order)."""
+    head, k_in, k_out = HEADS_A[0]
+    plan = [dict(prefix=param_prefix(head, 4), n_out=k_out, k_ref=256, transpose=1, n_tiles=8,
+                 k_steps=1, kmap=ident_kmap(k_out, 16), kmode=np.full(1, ACC, np.uint8))]
+    for li in (3, 2, 1):
+        plan.append(dict(prefix=param_prefix(head, li), n_out=256, k_ref=256, transpose=1, n_tiles=8,
+                         k_steps=16, kmap=ident_kmap(256, 256), kmode=np.full(16, ACC, np.uint8)))
+    plan.append(dict(prefix=param_prefix(head, 0), n_out=256, k_ref=k_in, transpose=1, n_tiles=9,
+                     k_steps=16, kmap=ident_kmap(256, 256), kmode=np.full(16, ACC, np.uint8),
+                     nmap=head_kmap(head)[:288]))
+    plan.append(dict(prefix="neural_sdf.mlp.linears.1", n_out=256, k_ref=256, transpose=1, n_tiles=8,
+                     k_steps=16, kmap=ident_kmap(256, 256), kmode=np.full(16, ACC, np.uint8)))
     return _with_offsets(plan)
 
 

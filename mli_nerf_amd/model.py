@@ -80,46 +80,63 @@ class _Encoding(torch.nn.Module):
 
 
 class NeuralSDF(torch.nn.Module):
-    """Parameter-compatible stand-in for neuralangelo/utils/modules.py:NeuralSDF (frozen in
-    stage b).  Attributes the trainers poke are kept (normal_eps, resolutions, ...)."""
+    """Parameter-compatible stand-in for neuralangelo/utils/modules.py:NeuralSDF.  Stage b:
+    frozen standalone tensors.  Stage a (``view`` given): the MLP parameters are views of the
+    model's flat trainable buffer and the hash table is trainable.  Attributes the trainers
+    poke are kept (normal_eps, resolutions, active_levels, anneal_levels, warm_up_end, ...)."""
 
-    def __init__(self, pcfg):
+    def __init__(self, pcfg, c2f=None, view=None):
         super().__init__()
         _, total = level_table(pcfg.levels, pcfg.log2T, pcfg.min_logres, pcfg.max_logres)
         self.tcnn_encoding = _Encoding(total * 8)
         k0 = 3 + pcfg.levels * 8
-        mlp = _MLP([WNLinear(torch.zeros(256, k0), torch.ones(256, 1), torch.zeros(256)),
-                    WNLinear(torch.zeros(256, 256), torch.ones(256, 1), torch.zeros(256))])
-        mlp.linear_sdf = PlainLinear(torch.zeros(1, 256), torch.zeros(1))
+        if view is None:
+            mlp = _MLP([WNLinear(torch.zeros(256, k0), torch.ones(256, 1), torch.zeros(256)),
+                        WNLinear(torch.zeros(256, 256), torch.ones(256, 1), torch.zeros(256))])
+            mlp.linear_sdf = PlainLinear(torch.zeros(1, 256), torch.zeros(1))
+        else:
+            pre = "neural_sdf.mlp."
+            mlp = _MLP([WNLinear(*(view(pre + "linears.%d.%s" % (li, n)) for n in ("weight_v", "weight_g", "bias")))
+                        for li in range(2)])
+            mlp.linear_sdf = PlainLinear(view(pre + "linear_sdf.weight"), view(pre + "linear_sdf.bias"))
+            for p in list(mlp.parameters()) + [self.tcnn_encoding.params]:
+                p.requires_grad_(True)
         self.mlp = mlp
+        self.levels = pcfg.levels
         g = np.exp((np.log(2 ** pcfg.max_logres) - np.log(2 ** pcfg.min_logres)) / (pcfg.levels - 1))
         self.growth_rate = g
         self.resolutions = [int(np.floor(2 ** pcfg.min_logres * g ** lv)) + 1 for lv in range(pcfg.levels)]
         self.normal_eps = 1.0 / self.resolutions[-1]
         self.active_levels = self.anneal_levels = pcfg.levels
         self.warm_up_end = 0
+        # coarse-to-fine (neuralangelo/configs/base.yaml:64-67; enabled in stage a)
+        self.c2f = c2f if c2f is not None and c2f.get("enabled", False) else None
 
     def set_normal_epsilon(self):
-        """modules.py:102-107 (coarse-to-fine disabled in stage b)."""
-        self.normal_eps = 1.0 / self.resolutions[-1]
+        """modules.py:102-107: tap epsilon = 1 / resolution of level anneal_levels - 1 under
+        coarse-to-fine, else of the finest level."""
+        res = self.resolutions[self.anneal_levels - 1] if self.c2f else self.resolutions[-1]
+        self.normal_eps = 1.0 / res
 
     def set_active_levels(self, current_iter=None):
-        self.active_levels = self.anneal_levels = len(self.resolutions)
+        """modules.py:97-100."""
+        if self.c2f is None or current_iter is None:
+            self.active_levels = self.anneal_levels = len(self.resolutions)
+            return
+        anneal = max((current_iter - self.warm_up_end) // self.c2f["step"], 1)
+        self.anneal_levels = min(self.levels, anneal)
+        self.active_levels = max(self.c2f["init_active_level"], self.anneal_levels)
 
 
 class LumenRGB(torch.nn.Module):
-    """Parameter layout of NeuralLumen/utils/modules.py:LumenRGB mode 'rgb_r_s'; the
-    tensors are views of the model's flat trainable buffer."""
+    """Parameter layout of NeuralLumen/utils/modules.py:LumenRGB -- mode 'rgb_r_s' (three
+    heads, stage b) or 'rgb' (the single ``mlp`` head, stage a); the tensors are views of the
+    model's flat trainable buffer."""
 
-    def __init__(self, flat):
+    def __init__(self, view, heads=layout.HEADS):
         super().__init__()
-        lay = {name: (shape, off) for name, shape, off in layout.trainable_layout()[0]}
-
-        def view(name):
-            shape, off = lay[name]
-            return flat[off:off + int(np.prod(shape))].view(*shape)
-
-        for head, _, _ in layout.HEADS:
+        self.network_mode = "rgb" if len(heads) == 1 else "rgb_r_s"
+        for head, _, _ in heads:
             lins = []
             for li in range(5):
                 pre = layout.param_prefix(head, li)
@@ -146,6 +163,9 @@ class _RenderHeads(torch.autograd.Function):
     @staticmethod
     def backward(ctx, d_rgb, d_o_r, d_o_s, d_o_re):
         model = ctx.model
+        if model.stage == "a":
+            raise NotImplementedError("stage-a gradients (geometry + hash table) run through the fused "
+                                      "Trainer.train_step (mli_nerf_amd.trainer), not torch autograd")
         grad = torch.zeros_like(model.flat)
         model.engine.backward(ctx.state, d_rgb, d_o_r, d_o_s, d_o_re, model.flat, model._sdf_l1(), grad)
         ctx.state = None
@@ -165,13 +185,29 @@ class Model(torch.nn.Module):
         self.anneal_end = self.pcfg.anneal_end
         self.progress = 0.0
         self.stratified = bool(cfg_model.render.stratified)
-        self.neural_sdf = NeuralSDF(self.pcfg)
-        n_train = layout.trainable_layout()[1]
+        mode = _cfg_get(cfg_model, "object.rgb.network_mode", None)
+        if mode not in (None, "rgb", "rgb_r_s"):
+            raise NotImplementedError("LumenRGB network_mode %r is outside the built hot path" % mode)
+        # 'rgb' (no network_mode, NeuralLumen/utils/modules.py:50-55): stage a -- every parameter
+        # trains (no partial_grad); 'rgb_r_s': stage b -- the heads train on frozen geometry
+        self.stage = "b" if mode == "rgb_r_s" else "a"
+        self._layout = {name: (shape, off) for name, shape, off in layout.trainable_layout(self.stage)[0]}
+        n_train = layout.trainable_layout(self.stage)[1]
         self.register_buffer("flat", torch.zeros(n_train), persistent=False)
         self.flat.requires_grad_(True)
-        self.neural_rgb = LumenRGB(self.flat)
-        self.s_var = torch.nn.Parameter(torch.tensor(float(cfg_model.object.s_var.init_val)),
-                                        requires_grad=False)
+        c2f = _cfg_get(cfg_model, "object.sdf.encoding.coarse2fine", None)
+        c2f = None if c2f is None else {k: c2f[k] for k in ("enabled", "init_active_level", "step") if k in c2f}
+        if self.stage == "a":
+            self.neural_sdf = NeuralSDF(self.pcfg, c2f, view=self._view)
+            self.neural_rgb = LumenRGB(self._view, layout.HEADS_A)
+            self.s_var = torch.nn.Parameter(self._view("s_var"), requires_grad=True)
+            with torch.no_grad():
+                self.s_var.fill_(float(cfg_model.object.s_var.init_val))
+        else:
+            self.neural_sdf = NeuralSDF(self.pcfg, c2f)
+            self.neural_rgb = LumenRGB(self._view)
+            self.s_var = torch.nn.Parameter(torch.tensor(float(cfg_model.object.s_var.init_val)),
+                                            requires_grad=False)
         if self.pcfg.bounding == "box":
             self.bounding_box_aabb = torch.tensor(self.pcfg.aabb)
         self.engine = None
@@ -179,39 +215,63 @@ class Model(torch.nn.Module):
         self.image_width = self.image_size_train[1]
 
     # -------------------------------------------------------------- parameter plumbing
+    def _view(self, name, flat=None):
+        shape, off = self._layout[name]
+        flat = self.flat if flat is None else flat
+        return flat.data[off:off + int(np.prod(shape))].view(shape)
+
+    def _layout_items(self):
+        """[(name, shape, offset)] of the flat trainable buffer."""
+        return layout.trainable_layout(self.stage)[0]
+
     def device(self):
         return self.flat.device
 
     def _apply(self, fn, recurse=True):
         super()._apply(fn, recurse)
-        # re-point the neural_rgb parameter views at the (possibly moved) flat buffer
+        # re-point the parameter views at the (possibly moved) flat buffer
         flat = self.flat.detach().requires_grad_(True)
         self._buffers["flat"] = flat
-        lay = {name: (shape, off) for name, shape, off in layout.trainable_layout()[0]}
-        for name, p in self.neural_rgb.named_parameters():
-            shape, off = lay["neural_rgb." + name]
-            p.data = flat.data[off:off + int(np.prod(shape))].view(*shape)
+        for name, p in self.named_parameters():
+            if name in self._layout:
+                p.data = self._view(name, flat)
         self.engine = None
         self._sdf_version = None
         return self
 
     def _sdf_l1(self):
+        if self.stage == "a":
+            return None  # packed from the flat buffer with the heads
         l1 = self.neural_sdf.mlp.linears[1]
         return (l1.weight_v.detach(), l1.weight_g.detach().reshape(-1), l1.bias.detach())
 
     def prepare(self):
-        """(Re)build the device weight images: SDF (once, frozen) + heads (every step)."""
+        """(Re)build the device weight images.  Stage b: SDF once (frozen) + heads every step.
+        Stage a: the fp16 table shadow when the table changed outside the fused AdamW (which
+        keeps it in sync), the SDF blocks and the heads every step; tap epsilon and the
+        coarse-to-fine level count from neural_sdf."""
         if self.engine is None:
-            self.engine = RenderEngine(self.pcfg, self.flat.device)
+            self.engine = RenderEngine(self.pcfg, self.flat.device, self.stage)
         sdf = self.neural_sdf
-        ver = tuple(p._version for p in sdf.parameters()) + tuple(p.data_ptr() for p in sdf.parameters())
-        if ver != self._sdf_version:
-            l0 = sdf.mlp.linears[0]
-            self.engine.load_sdf(sdf.tcnn_encoding.params.detach(), l0.weight_v.detach(),
-                                 l0.weight_g.detach().reshape(-1), l0.bias.detach(),
-                                 sdf.mlp.linear_sdf.weight.detach().reshape(-1), sdf.mlp.linear_sdf.bias.detach())
-            self._sdf_version = ver
-        self.engine.pack_heads(self.flat.detach(), self._sdf_l1())
+        eng = self.engine
+        eng.set_normal_eps(sdf.normal_eps)
+        eng.active_levels = int(sdf.active_levels)
+        l0 = sdf.mlp.linears[0]
+        pack_args = (l0.weight_v.detach(), l0.weight_g.detach().reshape(-1), l0.bias.detach(),
+                     sdf.mlp.linear_sdf.weight.detach().reshape(-1), sdf.mlp.linear_sdf.bias.detach())
+        if self.stage == "a":
+            table = sdf.tcnn_encoding.params
+            ver = (table._version, table.data_ptr())
+            if ver != self._sdf_version:
+                eng.load_table(table.detach())
+                self._sdf_version = ver
+            eng.pack_sdf(*pack_args)
+        else:
+            ver = tuple(p._version for p in sdf.parameters()) + tuple(p.data_ptr() for p in sdf.parameters())
+            if ver != self._sdf_version:
+                eng.load_sdf(sdf.tcnn_encoding.params.detach(), *pack_args)
+                self._sdf_version = ver
+        eng.pack_heads(self.flat.detach(), self._sdf_l1())
 
     # -------------------------------------------------------------- reference API
     def get_param_groups(self, cfg_optim):
@@ -251,6 +311,9 @@ class Model(torch.nn.Module):
                    gradients=fld["grad"].permute(1, 0, 2).reshape(1, R, N, 3),
                    hessians=None if fld["hess"] is None else fld["hess"].permute(1, 0, 2).reshape(1, R, N, 3),
                    opacity=None, gradient=None)
+        if self.stage == "a":  # mode 'rgb' has no intrinsic outputs (NeuralLumen/model.py:300-303)
+            for k in ("o_r", "o_s", "o_re"):
+                out.pop(k)
         if not self.training:
             out["opacity"] = comp["opacity"][None]
             out["gradient"] = comp["gradient"][None]

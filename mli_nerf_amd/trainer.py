@@ -101,11 +101,13 @@ class FusedAdamW:
         self.v = torch.zeros_like(flat.detach())
         self.step_count = 0
 
-    def step(self, grad, lr):
+    def step(self, grad, lr, p16=None):
+        """``p16``: fp16 tensor to receive a copy of the updated parameters (the hash table's
+        gather shadow), or None."""
         self.step_count += 1
         L.call("mli_adamw", L.AdamwArgs(L.ptr(self.flat.detach()), L.ptr(grad), L.ptr(self.m), L.ptr(self.v),
                                         self.flat.numel(), float(lr), self.betas[0], self.betas[1], self.eps,
-                                        self.wd, self.step_count))
+                                        self.wd, self.step_count, L.ptr(p16)))
 
     def state_dict(self):
         return {"step": self.step_count, "exp_avg": self.m, "exp_avg_sq": self.v, "lr": self.lr,
@@ -143,7 +145,17 @@ class Trainer:
         self.re_factors = (q["factor_negative"], q["factor_positive"], q["exponent_positive"])
         self._scratch = self._grad = None
         o = cfg.optim
+        self.stage = getattr(model, "stage", "b")
         self.optim = FusedAdamW(model.flat, lr=o.params.lr, weight_decay=o.params.weight_decay)
+        self.optim_table = None
+        if self.stage == "a":
+            # stage a trains the hash table too (one AdamW group, NeuralLumen/model.py:422-438)
+            self.optim_table = FusedAdamW(model.neural_sdf.tcnn_encoding.params, lr=o.params.lr,
+                                          weight_decay=o.params.weight_decay)
+            self.init_curvature = float(cfg.trainer.loss_weight.get("curvature", 0.0))
+            if model.neural_sdf.c2f is not None:   # neuralangelo/trainer.py:30-32
+                model.neural_sdf.warm_up_end = o.sched.warm_up_end
+        self._grad_table = None
         self.sched = o.sched
         self.current_iteration = 0
         self.current_epoch = 0
@@ -156,9 +168,21 @@ class Trainer:
                                                      tuple(s.two_steps), s.gamma)
 
     def _start_of_iteration(self):
-        """neuralangelo/trainer.py:65-76: progress restarts at 0 in stage b (no resume)."""
-        self.model.progress = self.current_iteration / self.cfg.max_iter
-        self.model.neural_sdf.set_normal_epsilon()
+        """neuralangelo/trainer.py:65-76: progress = iteration / max_iter (restarting at 0 in
+        stage b: no resume); coarse-to-fine active levels, tap epsilon and the curvature weight
+        schedule (get_curvature_weight, :56-63) when coarse-to-fine is on (stage a)."""
+        m = self.model
+        m.progress = self.current_iteration / self.cfg.max_iter
+        sdf = m.neural_sdf
+        if getattr(sdf, "c2f", None) is not None:
+            sdf.set_active_levels(self.current_iteration)
+            sdf.set_normal_epsilon()
+            if "curvature" in self.weights:
+                it, wue = self.current_iteration, self.sched.warm_up_end
+                self.weights["curvature"] = (it / wue * self.init_curvature if it <= wue else
+                                             self.init_curvature / sdf.growth_rate ** (sdf.anneal_levels - 1))
+        else:
+            sdf.set_normal_epsilon()
 
     def train_step(self, data, u=None, return_outputs=False):
         """One stage-b iteration.  Hot path: render -> fused losses + output gradients
@@ -167,6 +191,8 @@ class Trainer:
         reference's loss code on Model.forward's outputs)."""
         self._start_of_iteration()
         self.model.train()
+        if self.stage == "a":
+            return self.train_step_a(data, u, return_outputs)
         if not set(self.weights) <= FUSED_LOSSES:
             return self.train_step_autograd(data, u)
         m = self.model
@@ -204,6 +230,70 @@ class Trainer:
         self.optim.step(grad, self.lr())
         self.current_iteration += 1
         self.losses = {k: lv[i] for i, k in enumerate(LOSS_NAMES) if k in w}
+        self.losses["total"] = lv[5]
+        self.metrics["psnr"] = lv[6]
+        return m.outputs(st) if return_outputs else None
+
+    def _fused_losses(self, st, data, lv):
+        """mli_stage_b_loss: loss values + d total / d (rgb, o_r, o_s, o_re)."""
+        m, eng = self.model, self.model.engine
+        rays, dists, fld, hd, comp = st
+        N, R = dists.shape
+        d_rgb, d_o_r = eng._buf("d_rgb", (R, 3)), eng._buf("d_o_r", (R, 3))
+        d_o_s, d_o_re = eng._buf("d_o_s", (R, 1)), eng._buf("d_o_re", (R, 3))
+        if self._scratch is None or self._scratch.device != m.flat.device:
+            self._scratch = torch.zeros(16, device=m.flat.device)
+        w = self.weights
+        intr = "intrinsic" in w
+        L.call("mli_stage_b_loss", L.LossArgs(
+            R, N, L.ptr(comp["rgb"]), L.ptr(comp["o_r"]), L.ptr(comp["o_s"]), L.ptr(comp["o_re"]),
+            L.ptr(_c(data["image_sampled"])), L.ptr(_c(data.get("pseudo_ref_sampled")) if intr else None),
+            L.ptr(_c(data.get("pseudo_sha_sampled")) if intr else None),
+            L.ptr(_c(data.get("pseudo_visibility_certainty_sampled")) if intr else None),
+            L.ptr(rays["outside"]), L.ptr(fld["grad"]) if "eikonal" in w else None,
+            L.ptr(fld["hess"]) if "curvature" in w else None,
+            w.get("render", 0.0), w.get("eikonal", 0.0), w.get("curvature", 0.0), w.get("intrinsic", 0.0),
+            w.get("regularize_re", 0.0), self.ranges[0][0], self.ranges[0][1], self.ranges[1][0],
+            self.ranges[1][1], self.intr_factors[0], self.intr_factors[1], *self.re_factors,
+            L.ptr(d_rgb), L.ptr(d_o_r), L.ptr(d_o_s), L.ptr(d_o_re), L.ptr(lv), L.ptr(self._scratch)))
+        return d_rgb, d_o_r, d_o_s, d_o_re
+
+    def compute_grads_a(self, data, u=None):
+        """Stage-a forward + fused losses + backward (no optimizer step): fills self._grad (flat
+        MLP buffer incl. s_var) and self._grad_table; returns (render state, loss values)."""
+        m = self.model
+        m.prepare()
+        m.image_width = m.image_size_train[1]
+        st = m.engine.render(data, m.s_var.detach(), m.progress, True, u=m.stratified_uniforms(data, u),
+                             W=m.image_width)
+        m._last_state = st
+        lv = torch.empty(8, device=m.flat.device)
+        d_rgb = self._fused_losses(st, data, lv)[0]
+        if self._grad is None or self._grad.device != m.flat.device:
+            self._grad = torch.empty_like(m.flat.detach())
+        table = m.neural_sdf.tcnn_encoding.params
+        if self._grad_table is None or self._grad_table.device != table.device:
+            self._grad_table = torch.empty_like(table.detach())
+        m.engine.backward_a(st, d_rgb, m.flat.detach(), self._grad, self._grad_table,
+                            self.weights.get("eikonal", 0.0), self.weights.get("curvature", 0.0), m.progress)
+        return st, lv
+
+    def train_step_a(self, data, u=None, return_outputs=False):
+        """One stage-a iteration (syn_hotdog_a): render -> fused losses (render, eikonal,
+        curvature) -> geometry backward (composite, head, SDF MLP of the 5 points, hash-grid
+        scatter) -> all-reduce -> fused AdamW on the flat MLP buffer and on the hash table
+        (which also refreshes the fp16 gather shadow)."""
+        m = self.model
+        st, lv = self.compute_grads_a(data, u)
+        eng = m.engine
+        grad = reduce_gradients(self._grad, self.world_size)
+        gtab = reduce_gradients(self._grad_table, self.world_size)
+        m.flat.grad = grad
+        lr = self.lr()
+        self.optim.step(grad, lr)
+        self.optim_table.step(gtab, lr, p16=eng.table16)
+        self.current_iteration += 1
+        self.losses = {k: lv[i] for i, k in enumerate(LOSS_NAMES) if k in self.weights}
         self.losses["total"] = lv[5]
         self.metrics["psnr"] = lv[6]
         return m.outputs(st) if return_outputs else None
