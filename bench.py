@@ -33,13 +33,33 @@ HEAD_IN = (294, 262, 278)
 HEAD_OUT = (3, 3, 1)
 
 
-def kernel_flops(name, R, N, Nc, Nf, H):
-    """Algorithmic MLP FLOPs (2*MAC) per launch of each MFMA kernel."""
+def progress(msg):
+    """Progress line on stderr (long runs must keep writing: the GPU box kills silent ones)."""
+    print("[bench] " + msg, file=sys.stderr, flush=True)
+
+
+def kernel_flops(name, R, N, Nc, Nf, H, stage="b"):
+    """Algorithmic MLP FLOPs (2*MAC) per step (unit) of each MFMA kernel.
+    Stage a (LumenRGB mode 'rgb': the single 294 -> 3 head, geometry trained) adds the
+    geometry backward: mli_geo_bwd (head dX chain + W0^T to feat/normal + SDF layer 1 dX),
+    mli_sdf_bwd (layer 0 recomputed and d enc = W0_enc^T dZ0 for the 5 points) and the two
+    dW launches (S samples: head + SDF layer 1; 5S samples: SDF layer 0)."""
     S = R * N
     sdf_point = 2 * ((3 + 128) * HIDDEN + HIDDEN)                  # layer 0 + sdf head
-    heads_fwd = sum(k * HIDDEN + 3 * HIDDEN * HIDDEN + HIDDEN * o for k, o in zip(HEAD_IN, HEAD_OUT))
+    head_in, head_out = (HEAD_IN[:1], HEAD_OUT[:1]) if stage == "a" else (HEAD_IN, HEAD_OUT)
+    heads_fwd = sum(k * HIDDEN + 3 * HIDDEN * HIDDEN + HIDDEN * o for k, o in zip(head_in, head_out))
     if name == "mli_rgb_fwd":
         return 2 * S * (HIDDEN * HIDDEN + heads_fwd)               # SDF layer 1 (feat) + heads
+    if name == "mli_sdf:field":
+        return 5 * S * sdf_point
+    if stage == "a":
+        if name == "mli_geo_bwd":  # W4^T..W1^T, W0^T onto feat + normal, W1sdf^T
+            return 2 * S * (HIDDEN * 3 + 3 * HIDDEN * HIDDEN + HIDDEN * (HIDDEN + 3) + HIDDEN * HIDDEN)
+        if name == "mli_sdf_bwd":  # per point: z0 recompute (131 x 256) + d enc (256 -> 128)
+            return 2 * 5 * S * ((3 + 128) * HIDDEN + 128 * HIDDEN)
+        if name == "mli_wgrad":    # both launches: head + SDF layer 1 over S, SDF layer 0 over 5S
+            return 2 * S * (heads_fwd + HIDDEN * HIDDEN) + 2 * 5 * S * HIDDEN * (3 + 128)
+        return 0
     if name == "mli_rgb_bwd":
         return 2 * S * sum(HIDDEN * o + 3 * HIDDEN * HIDDEN for o in HEAD_OUT)
     if name == "mli_wgrad":
@@ -50,8 +70,6 @@ def kernel_flops(name, R, N, Nc, Nf, H):
         return 2 * S * HIDDEN * sum(HEAD_IN)
     if name == "mli_wgrad:thin":   # dW of the output layers (3 / 3 / 1 rows)
         return 2 * S * HIDDEN * sum(HEAD_OUT)
-    if name == "mli_sdf:field":
-        return 5 * S * sdf_point
     return 0
 
 
@@ -76,8 +94,9 @@ def pmc_traffic(kernel, n_units_check):
             "traffic_source": os.path.relpath(PMC_SUMMARY, HERE) + " (rocprofv3 --pmc, separate passes)"}
 
 
-def kernel_table(prof, n_units, R, N, fine):
-    """Per-call-name HIP-event timings -> table + roofline record of the dominant MFMA call."""
+def kernel_table(prof, n_units, R, N, fine, stage="b"):
+    """Per-call-name HIP-event timings -> table + roofline record of the dominant MFMA call
+    (FLOPs per step / kernel time per step; = per launch for the one-launch kernels)."""
     kernels = {}
     for name, e0, e1 in prof or []:
         k = kernels.setdefault(name, [0.0, 0])
@@ -85,22 +104,23 @@ def kernel_table(prof, n_units, R, N, fine):
         k[1] += 1
     ktab = {n: {"ms_per_launch": v[0] / v[1], "launches_per_unit": v[1] / n_units,
                 "ms_per_unit": v[0] / n_units} for n, v in sorted(kernels.items(), key=lambda kv: -kv[1][0])}
+    flops = lambda n: kernel_flops(n, R, N, 64, fine, 4, stage)  # noqa: E731
     roof = None
-    mfma = [n for n in ktab if kernel_flops(n, R, N, 64, fine, 4) > 0]
+    mfma = [n for n in ktab if flops(n) > 0]
     if mfma:
         dom = max(mfma, key=lambda n: ktab[n]["ms_per_unit"])
-        fl = kernel_flops(dom, R, N, 64, fine, 4)
-        achieved = fl / (ktab[dom]["ms_per_launch"] * 1e-3) / 1e12
+        fl = flops(dom)
+        achieved = fl / (ktab[dom]["ms_per_unit"] * 1e-3) / 1e12
         roof = {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_F16_TFLOPS, 4), "traffic": None,
-                "flops_per_launch": fl}
-        pmc = pmc_traffic(dom, n_units_check=R * N)
+                "flops_per_launch": int(fl / ktab[dom]["launches_per_unit"])}
+        pmc = pmc_traffic(dom, n_units_check=R * N) if stage == "b" else None
         if pmc:
             roof.update(pmc)
         for n in ktab:
-            f = kernel_flops(n, R, N, 64, fine, 4)
+            f = flops(n)
             if f:
-                ktab[n]["tflops"] = round(f / (ktab[n]["ms_per_launch"] * 1e-3) / 1e12, 2)
+                ktab[n]["tflops"] = round(f / (ktab[n]["ms_per_unit"] * 1e-3) / 1e12, 2)
     return ktab, roof
 
 
@@ -221,15 +241,22 @@ def oracle_cfg(cfg):
                             aabb=tuple(cfg.data.get("bounding_box_aabb", (-1, -1, -1, 1, 1, 1))))
 
 
-def cpu_baseline(cfg, R_cpu, steps, threads):
+def cpu_baseline(cfg, R_cpu, steps, threads, stage_a=None):
     """The CPU oracle (fp32 PyTorch restatement of the reference path) timed on the host:
-    stage-b forward + losses + backward on R_cpu rays of the same workload."""
+    forward + losses + backward on R_cpu rays of the same workload (stage b: into the heads;
+    stage a, ``stage_a`` = (active_levels, anneal_levels, curvature weight, progress): into
+    every parameter incl. the hash table)."""
     from mli_nerf_amd import synthetic
     from oracle import render as o_render
     torch.set_num_threads(threads)
-    sd = synthetic.make_state_dict(log2T=22)
-    sd = {k: v.requires_grad_(k.startswith("neural_rgb")) for k, v in sd.items()}
     pcfg = oracle_cfg(cfg)
+    if stage_a is not None:
+        sd = synthetic.make_state_dict(log2T=22, heads="rgb")
+        sd = {k: v.requires_grad_(True) for k, v in sd.items()}
+        pcfg.rgb_mode, pcfg.active_levels, pcfg.anneal_levels = "rgb", stage_a[0], stage_a[1]
+    else:
+        sd = synthetic.make_state_dict(log2T=22)
+        sd = {k: v.requires_grad_(k.startswith("neural_rgb")) for k, v in sd.items()}
     Hh, W = cfg.data.train.image_size
     data = synthetic.make_batch(R_cpu, H=Hh, W=W, frame=0, seed=7)
     u = synthetic.stratified_uniforms(R_cpu, pcfg.n_coarse, seed=7)
@@ -237,17 +264,23 @@ def cpu_baseline(cfg, R_cpu, steps, threads):
     out = psnr = None
     for i in range(steps + 2):  # 2 untimed warm-up steps
         t0 = time.perf_counter()
-        out = o_render.forward(sd, pcfg, data, u=u, training=True, progress=0.0, width=W, height=Hh)
-        total, _, psnr = o_render.stage_b_losses(out, data, pcfg)
+        if stage_a is not None:
+            out = o_render.forward(sd, pcfg, data, u=u, training=True, progress=stage_a[3], width=W, height=Hh)
+            total, _, psnr = o_render.stage_a_losses(out, data, stage_a[2])
+        else:
+            out = o_render.forward(sd, pcfg, data, u=u, training=True, progress=0.0, width=W, height=Hh)
+            total, _, psnr = o_render.stage_b_losses(out, data, pcfg)
         total.backward()
         for v in sd.values():
             v.grad = None
         if i > 1:
             times.append(time.perf_counter() - t0)
+        progress("cpu baseline step %d/%d: %.2f s" % (i + 1, steps + 2, time.perf_counter() - t0))
     t = sum(times) / len(times)
     return dict(value=R_cpu / t, unit="rays/s", cores=threads, kind="port",
-                sample="oracle fwd+bwd stage-b, %d rays x %d samples, full hash table, %d timed steps "
-                       "after 2 warm-up, torch fp32 on %d host threads" % (R_cpu, pcfg.n_samples, steps, threads),
+                sample="oracle fwd+bwd stage-%s, %d rays x %d samples, full hash table, %d timed steps "
+                       "after 2 warm-up, torch fp32 on %d host threads" % ("a" if stage_a else "b", R_cpu,
+                                                                          pcfg.n_samples, steps, threads),
                 s_per_step=t), data, u, float(psnr)
 
 
@@ -268,6 +301,9 @@ def main():
     ap.add_argument("--frames", type=int, default=4, help="infer: frames timed (after --warmup frames)")
     ap.add_argument("--size", type=int, default=800, help="infer: frame is size x size")
     ap.add_argument("--chunk", type=int, default=20000, help="infer: rand_rays_val")
+    ap.add_argument("--iteration", type=int, default=100000,
+                    help="stage a (--config syn_hotdog_a): training iteration (sets the coarse-to-fine "
+                         "levels, tap epsilon and curvature weight; >= 80000: all 16 levels active)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -289,9 +325,13 @@ def main():
 
     cfg = preset(args.config, rays=args.rays, n_fine=args.fine)
     model = Model(cfg.model, cfg.data)
-    model.load_state_dict(synthetic.make_state_dict(log2T=22, seed=0))
+    stage_a = model.stage == "a"
+    model.load_state_dict(synthetic.make_state_dict(log2T=22, seed=0, heads="rgb" if stage_a else "rgb_r_s"))
     model = model.to(dev)
     trainer = Trainer(cfg, model, world_size=world)
+    if stage_a:
+        # steady state of stage a: past the coarse-to-fine ramp (all 16 levels active)
+        trainer.current_iteration = args.iteration
     Hh, W = cfg.data.train.image_size
     batch = {k: v.to(dev) for k, v in synthetic.make_batch(args.rays, H=Hh, W=W, frame=rank).items()}
     R, N = args.rays, model.pcfg.n_samples
@@ -304,6 +344,7 @@ def main():
     for _ in range(args.warmup):
         trainer.train_step(batch)
     torch.cuda.synchronize()
+    progress("warm-up done (%d steps)" % args.warmup)
     barrier()
     torch.cuda.synchronize()
     if not args.no_kernel_timing:
@@ -315,6 +356,7 @@ def main():
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    progress("timed steps done: %.3f ms/step" % (elapsed / args.steps * 1e3))
     prof, L.PROFILE = L.PROFILE, None
     if world > 1:
         import torch.distributed as dist
@@ -324,7 +366,7 @@ def main():
     psnr = trainer.metrics["psnr"].item()
     loss = trainer.losses["total"].item()
 
-    ktab, roof = kernel_table(prof, args.steps, R, N, args.fine)
+    ktab, roof = kernel_table(prof, args.steps, R, N, args.fine, model.stage)
 
     step_ms = elapsed / args.steps * 1e3
     value = R * world * args.steps / elapsed
@@ -334,14 +376,25 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f16 MFMA (fp32 accumulate) / fp32",
         "data": "synthetic (seeded cameras/lights/labels, random-init weights, full 2^22 hash table)",
-        "config": {"workload": "%s stage-b train step" % args.config, "rays_per_gpu": R, "samples_per_ray": N,
-                   "global_rays": R * world, "image": [Hh, W], "parallelism": "dp%d" % world},
+        "config": {"workload": "%s stage-%s train step" % (args.config, model.stage), "rays_per_gpu": R,
+                   "samples_per_ray": N, "global_rays": R * world, "image": [Hh, W], "parallelism": "dp%d" % world},
         "psnr": round(psnr, 4), "loss": round(loss, 6),
         "roofline": roof, "kernels": ktab,
-        "mfma_tflops_step": round(sum(kernel_flops(n, R, N, 64, args.fine, 4) for n in ktab) /
+        "mfma_tflops_step": round(sum(kernel_flops(n, R, N, 64, args.fine, 4, model.stage) for n in ktab) /
                                   (step_ms * 1e-3) / 1e12, 2),
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if stage_a:
+        sdf = model.neural_sdf
+        result["config"].update(iteration=trainer.current_iteration - 1, active_levels=int(sdf.active_levels),
+                                curvature_weight=trainer.weights["curvature"])
+    if rank == 0 and world == 1 and not args.no_cpu and stage_a:
+        threads = min(16, os.cpu_count() or 1)
+        sdf = model.neural_sdf
+        sa = (int(sdf.active_levels), int(sdf.anneal_levels), trainer.weights["curvature"], model.progress)
+        cb, data_cpu, u_cpu, psnr_cpu = cpu_baseline(cfg, args.cpu_rays, args.cpu_steps, threads, stage_a=sa)
+        result["cpu_baseline"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in cb.items()}
+        result["speedup_vs_cpu"] = round(value / cb["value"], 1)
+    elif rank == 0 and world == 1 and not args.no_cpu:
         threads = min(16, os.cpu_count() or 1)
         cb, data_cpu, u_cpu, psnr_cpu = cpu_baseline(cfg, args.cpu_rays, args.cpu_steps, threads)
         result["cpu_baseline"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in cb.items()}

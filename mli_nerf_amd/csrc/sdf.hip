@@ -660,11 +660,20 @@ __global__ __launch_bounds__(MLP_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_arg
 // Hash-grid backward, level-outer like encode5_kernel: lane (c, h) = sample c, level 2qq+h.
 // The center's 8 corners take the weighted d enc of every point in the center's cell (one
 // fp32 atomic per corner feature); a tap in another cell scatters its own 64.
-__global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
+// lv_only >= 0: one level per launch (level-major over the whole sample set, so the atomic
+// working set is one level's gradient -- <= 2^22 entries x 32 B = 128 MiB, Infinity-Cache
+// sized -- instead of the whole 1.46 GB table); each lane half then takes its own tile.
+__global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a, int lv_only) {
+  // per wave: up to 64 run totals (64 floats) + their 8 corner slots, for the coalesced scatter
+  __shared__ __attribute__((aligned(16))) float s_vals[4][64 * 64];
+  __shared__ uint32_t s_slot[4][64 * 8];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* tvals = s_vals[wave];
+  uint32_t* tslot = s_slot[wave];
   const int c = lane & 31, h = lane >> 5;
   const int S = a.R * a.N;
-  const int tile = blockIdx.x * 4 + wave;
+  const bool single = lv_only >= 0;
+  const int tile = single ? (blockIdx.x * 4 + wave) * 2 + h : blockIdx.x * 4 + wave;
   if (tile >= S / 32) return;
   const int m = tile * 32 + c;
   const int r = m / a.N, k = m - r * a.N;
@@ -675,12 +684,21 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
   for (int p = 0; p < TAPS; ++p)
 #pragma unroll
     for (int d = 0; d < 3; ++d) x[p][d] = (q[p][d] + 2.0f) * 0.25f;
-  const float* src = a.d_enc + ((size_t)tile * TAPS * 8) * 512 + lane * 8;
+  const int lane_src = single ? c + 32 * (lv_only & 1) : lane;
+  const float* src = a.d_enc + ((size_t)tile * TAPS * 8) * 512 + lane_src * 8;
+  const int n_it = single ? 1 : 8;
 #pragma unroll 1
-  for (int qq = 0; qq < 8; ++qq) {
-    if (2 * qq >= a.active_levels) break;
-    const int lv = 2 * qq + h;
-    if (lv >= a.active_levels) continue;
+  for (int it = 0; it < n_it; ++it) {
+    const int qq = single ? lv_only >> 1 : it;
+    if (!single && 2 * qq >= a.active_levels) break;
+    const int lv = single ? lv_only : 2 * qq + h;
+    // a masked level stays in the loop with zero contributions: the coalesced scatter needs
+    // every lane of the wave (lane j adds corner j/8 of a run)
+    bool lv_on = lv < a.active_levels;
+#ifdef MLI_EXP_LEVELS_LO  // experiment builds (tools/kbench_a.py): time a level range only
+    lv_on = lv_on && lv >= MLI_EXP_LEVELS_LO && lv < MLI_EXP_LEVELS_HI;
+#endif
+    if (!__any(lv_on)) continue;
     const LevelP P = level_params(a.levels, lv);
     const bool dense = level_dense(a.levels, lv);
     const uint32_t r2 = P.res * P.res;
@@ -709,8 +727,12 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
       for (int cc = 0; cc < 8; ++cc) {
         const uint32_t idx = index_of(g[0] + (cc & 1), g[1] + ((cc >> 1) & 1), g[2] + ((cc >> 2) & 1));
         float* dstp = a.d_table + (size_t)(P.offset + idx) * 8;
+#ifdef MLI_EXP_NO_ATOMICS
+        if (G[cc][0] == 1234.5f) dstp[0] = G[cc][1];
+#else
 #pragma unroll
         for (int f = 0; f < 8; ++f) unsafeAtomicAdd(dstp + f, G[cc][f]);
+#endif
       }
     };
     uint32_t g0[3];
@@ -720,7 +742,8 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
     {
       const f32x4 lo = *reinterpret_cast<const f32x4*>(src + (size_t)qq * 512);
       const f32x4 hi = *reinterpret_cast<const f32x4*>(src + (size_t)qq * 512 + 4);
-      const float d[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const float on = lv_on ? 1.0f : 0.0f;
+      const float d[8] = {lo[0] * on, lo[1] * on, lo[2] * on, lo[3] * on, hi[0] * on, hi[1] * on, hi[2] * on, hi[3] * on};
 #pragma unroll
       for (int cc = 0; cc < 8; ++cc) {
         const float w = weight(pos0, cc);
@@ -728,12 +751,102 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
         for (int f = 0; f < 8; ++f) G[cc][f] = w * d[f];
       }
     }
+    // Run-segmented reduction (see below) over the 32 consecutive samples of the lane half:
+    // lanes sharing `key` cell form contiguous runs along the ray; the run's last lane holds
+    // the run total of V and (if the run carries any contribution) scatters it.
+    const int c0 = lane & 31;
+    auto run_scatter = [&](const uint32_t (&cellk)[3], float (&V)[8][8], bool mine) MLI_LAMBDA_FI {
+      // lanes without a contribution get a lane-unique key: singleton runs that never scatter
+      // and never lengthen the scan
+      const uint32_t key[3] = {mine ? cellk[0] : 0xFFFFFFFFu, mine ? cellk[1] : (uint32_t)lane,
+                               mine ? cellk[2] : 0xFFFFFFFFu};
+      const uint32_t px = __shfl_up(key[0], 1), py = __shfl_up(key[1], 1), pz = __shfl_up(key[2], 1);
+      const bool head = c0 == 0 || px != key[0] || py != key[1] || pz != key[2];
+      int start = head ? c0 : 0;  // first lane of this lane's run: max-scan of the heads
+#pragma unroll
+      for (int d = 1; d < 32; d <<= 1) {
+        const int o = __shfl_up(start, d);
+        if (c0 >= d) start = max(start, o);
+      }
+      // any lane of the run contributing (runs without contributions issue nothing)
+      const uint64_t bal = __ballot(mine);
+      const uint32_t hb = (uint32_t)(bal >> (32 * h));
+      const uint32_t upto = c0 == 31 ? 0xFFFFFFFFu : ((2u << c0) - 1u);
+      const uint32_t from = ~((1u << start) - 1u);
+      const bool any = (hb & upto & from) != 0u;
+      if (!__any(any)) return;
+      // scan steps only up to the longest run of the wave (fine levels: mostly 1-sample runs)
+      int span = c0 - start;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) span = max(span, __shfl_xor(span, o));
+#pragma unroll 1
+      for (int d = 1; d <= span; d <<= 1) {
+        const bool take = c0 - d >= start;
+#pragma unroll
+        for (int cc = 0; cc < 8; ++cc)
+#pragma unroll
+          for (int f = 0; f < 8; ++f) {
+            const float o = __shfl_up(V[cc][f], d);
+            V[cc][f] += take ? o : 0.0f;
+          }
+      }
+      const uint32_t nx = __shfl_down(key[0], 1), ny = __shfl_down(key[1], 1), nz = __shfl_down(key[2], 1);
+      const bool tail = (c0 == 31 || nx != key[0] || ny != key[1] || nz != key[2]) && any;
+#ifdef MLI_EXP_LANE_ATOMICS
+      if (tail) scatter(cellk, V);
+#else
+      // Coalesced scatter: the run totals go through LDS so one atomic instruction adds one
+      // run's 8 corners x 8 features with 8 consecutive lanes per corner (one 32 B L2 request
+      // per corner instead of 8 -- atomics here are request-rate bound, tools/atomic_bench.hip)
+      const uint64_t tb = __ballot(tail);
+      const int rank = __popcll(tb & ((1ull << lane) - 1ull));
+      const int ntail = __popcll(tb);
+      if (tail) {
+        f32x4* vd = reinterpret_cast<f32x4*>(tvals + rank * 64);
+#pragma unroll
+        for (int cc = 0; cc < 8; ++cc) {
+          vd[2 * cc] = f32x4{V[cc][0], V[cc][1], V[cc][2], V[cc][3]};
+          vd[2 * cc + 1] = f32x4{V[cc][4], V[cc][5], V[cc][6], V[cc][7]};
+          tslot[rank * 8 + cc] =
+              P.offset + index_of(cellk[0] + (cc & 1), cellk[1] + ((cc >> 1) & 1), cellk[2] + ((cc >> 2) & 1));
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // 4 runs per round: their LDS reads issue together (latency overlapped)
+#pragma unroll 1
+      for (int i0 = 0; i0 < ntail; i0 += 4) {
+        float v[4];
+        uint32_t slot[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i = min(i0 + u, 63);
+          v[u] = tvals[i * 64 + lane];
+          slot[u] = tslot[i * 8 + (lane >> 3)];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (i0 + u >= ntail) break;
+#ifdef MLI_EXP_NO_ATOMICS
+          if (v[u] == 1234.5f) a.d_table[(size_t)slot[u] * 8 + (lane & 7)] = v[u];
+#else
+          if (v[u] != 0.0f) unsafeAtomicAdd(a.d_table + (size_t)slot[u] * 8 + (lane & 7), v[u]);
+#endif
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
+    };
 #pragma unroll 1
     for (int p = 1; p < TAPS; ++p) {
       const float* sp = src + ((size_t)p * 8 + qq) * 512;
       const f32x4 lo = *reinterpret_cast<const f32x4*>(sp);
       const f32x4 hi = *reinterpret_cast<const f32x4*>(sp + 4);
-      const float d[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const float on = lv_on ? 1.0f : 0.0f;
+      const float d[8] = {lo[0] * on, lo[1] * on, lo[2] * on, lo[3] * on, hi[0] * on, hi[1] * on, hi[2] * on, hi[3] * on};
       float xp[3] = {x[0][0], x[0][1], x[0][2]};
 #pragma unroll
       for (int j = 1; j < TAPS; ++j) {
@@ -745,25 +858,32 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
       uint32_t g[3];
       float pos[3];
       cell(xp, g, pos);
-      if (g[0] == g0[0] && g[1] == g0[1] && g[2] == g0[2]) {
+      const bool same = g[0] == g0[0] && g[1] == g0[1] && g[2] == g0[2];
+      float T[8][8];
 #pragma unroll
-        for (int cc = 0; cc < 8; ++cc) {
-          const float w = weight(pos, cc);
+      for (int cc = 0; cc < 8; ++cc) {
+        const float w = weight(pos, cc);
 #pragma unroll
-          for (int f = 0; f < 8; ++f) G[cc][f] = fmaf(w, d[f], G[cc][f]);
+        for (int f = 0; f < 8; ++f) {
+          if (same) {
+            G[cc][f] = fmaf(w, d[f], G[cc][f]);
+            T[cc][f] = 0.0f;
+          } else {
+            T[cc][f] = w * d[f];
+          }
         }
-      } else {
-        float T[8][8];
-#pragma unroll
-        for (int cc = 0; cc < 8; ++cc) {
-          const float w = weight(pos, cc);
-#pragma unroll
-          for (int f = 0; f < 8; ++f) T[cc][f] = w * d[f];
-        }
-        scatter(g, T);
       }
+#ifndef MLI_EXP_NO_TAP_SCATTER
+      // a tap outside the center's cell: reduced over the runs of its own cell
+      if (__any(!same && lv_on)) run_scatter(g, T, !same && lv_on);
+#endif
     }
-    scatter(g0, G);
+    // Samples of a wave are 32 consecutive depths of one ray: lanes sharing the center cell
+    // form contiguous runs (a ray crosses a cell once).  Segmented inclusive scan of the 64
+    // corner-feature sums over each run (within the lane half = one level), then only the
+    // run's last lane issues the atomics -- coarse levels and the clustered fine samples
+    // collapse to a few atomics per cell instead of one per sample.
+    run_scatter(g0, G, lv_on);
   }
 }
 
@@ -829,7 +949,12 @@ extern "C" int mli_sdf_bwd(const mli_sdf_bwd_args* a, mli_stream_t s) {
 extern "C" int mli_hash_bwd(const mli_hash_bwd_args* a, mli_stream_t s) {
   const int S = a->R * a->N;
   if (S <= 0) return 0;
-  if (S % 32 != 0 || !a->d_enc || !a->d_table) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(hash_bwd_kernel, dim3((S / 32 + 3) / 4), dim3(256), 0, (hipStream_t)s, *a);
+  if (S % 64 != 0 || !a->d_enc || !a->d_table) return (int)hipErrorInvalidValue;
+#ifdef MLI_EXP_LEVEL_MAJOR  // measured slower (17.8 vs 15.7 ms at 4096 x 128): kept as an experiment
+  for (int lv = 0; lv < a->active_levels && lv < MLI_LEVELS; ++lv)
+    hipLaunchKernelGGL(hash_bwd_kernel, dim3((S / 64 + 3) / 4), dim3(256), 0, (hipStream_t)s, *a, lv);
+#else
+  hipLaunchKernelGGL(hash_bwd_kernel, dim3((S / 32 + 3) / 4), dim3(256), 0, (hipStream_t)s, *a, -1);
+#endif
   MLI_LAUNCH_CHECK();
 }
