@@ -94,9 +94,10 @@ def pmc_traffic(kernel, n_units_check):
             "traffic_source": os.path.relpath(PMC_SUMMARY, HERE) + " (rocprofv3 --pmc, separate passes)"}
 
 
-def kernel_table(prof, n_units, R, N, fine, stage="b"):
+def kernel_table(prof, n_units, R, N, fine, stage="b", per_launch=False):
     """Per-call-name HIP-event timings -> table + roofline record of the dominant MFMA call
-    (FLOPs per step / kernel time per step; = per launch for the one-launch kernels)."""
+    (FLOPs per step / kernel time per step; = per launch for the one-launch kernels).
+    per_launch: kernel_flops(R) counts one launch (inference chunks of R rays)."""
     kernels = {}
     for name, e0, e1 in prof or []:
         k = kernels.setdefault(name, [0.0, 0])
@@ -104,7 +105,9 @@ def kernel_table(prof, n_units, R, N, fine, stage="b"):
         k[1] += 1
     ktab = {n: {"ms_per_launch": v[0] / v[1], "launches_per_unit": v[1] / n_units,
                 "ms_per_unit": v[0] / n_units} for n, v in sorted(kernels.items(), key=lambda kv: -kv[1][0])}
-    flops = lambda n: kernel_flops(n, R, N, 64, fine, 4, stage)  # noqa: E731
+    def flops(n):
+        f = kernel_flops(n, R, N, 64, fine, 4, stage)
+        return f * ktab[n]["launches_per_unit"] if per_launch and n in ktab else f
     roof = None
     mfma = [n for n in ktab if flops(n) > 0]
     if mfma:
@@ -171,7 +174,7 @@ def run_infer(args, world, rank, dev):
     n_pix = size * size
     value = n_pix * args.frames / elapsed
     R_chunk = min(args.chunk, -(-n_pix // world))
-    ktab, roof = kernel_table(prof, args.frames, R_chunk, N, args.fine)
+    ktab, roof = kernel_table(prof, args.frames, R_chunk, N, args.fine, per_launch=True)
     result = {
         "metric": "rays/sec, syn_hotdog_b video_train inference %dx%d full frame (configs[4])" % (size, size),
         "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": args.frames,

@@ -311,6 +311,8 @@ typedef struct {
   uint16_t* x0_rows;      /* [131][5S] fp16 layer-0 input rows (p 0..2, enc 3..130); this writes rows 0..2 */
   float* dw_sdf;          /* [256] scaled, atomics (caller zeroes) */
   float* db_sdf;          /* [1] scaled, atomics (caller zeroes) */
+  const float* d_grad_ext; /* optional [N][R][3] d loss / d gradients from outside (autograd) */
+  const float* d_hess_ext; /* optional [N][R][3] d loss / d hessians from outside (autograd) */
 } mli_sdf_bwd_args;
 int mli_sdf_bwd(const mli_sdf_bwd_args* a, mli_stream_t s);
 

@@ -138,7 +138,7 @@ class SdfBwdArgs(C.Structure):
                 ("grad", P), ("hess", P), ("d_sdf", P), ("d_grad", P), ("d_nrm", P), ("dh0_frag", P), ("enc", P),
                 ("wsdf", P), ("wsdf_t", P), ("eps", F32), ("grad_den", F32), ("hess_den", F32),
                 ("w_eikonal", F32), ("w_curvature", F32), ("grad_scale", F32), ("d_enc", P), ("dz0_frag", P),
-                ("x0_rows", P), ("dw_sdf", P), ("db_sdf", P)]
+                ("x0_rows", P), ("dw_sdf", P), ("db_sdf", P), ("d_grad_ext", P), ("d_hess_ext", P)]
 
 
 class PackSdfTArgs(C.Structure):

@@ -522,6 +522,9 @@ __global__ __launch_bounds__(MLP_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_arg
     const bool out = a.outside[r] != 0;
     const float g0 = a.grad[3 * slot], g1 = a.grad[3 * slot + 1], g2 = a.grad[3 * slot + 2];
     float dg0 = a.d_grad[3 * slot], dg1 = a.d_grad[3 * slot + 1], dg2 = a.d_grad[3 * slot + 2];
+    if (a.d_grad_ext) {  // autograd: d loss / d gradients of the caller's own loss terms
+      dg0 += a.d_grad_ext[3 * slot]; dg1 += a.d_grad_ext[3 * slot + 1]; dg2 += a.d_grad_ext[3 * slot + 2];
+    }
     const float gn = sqrtf((g0 * g0 + g1 * g1) + g2 * g2);
     if (!out && gn > 0.f) {  // eikonal: mean((|g| - 1)^2 * !outside)
       const float e = (gn - 1.0f) * (gn - 1.0f);
@@ -546,6 +549,8 @@ __global__ __launch_bounds__(MLP_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_arg
       const float lap = (a.hess[3 * slot] + a.hess[3 * slot + 1]) + a.hess[3 * slot + 2];
       if (isfinite(lap) && lap != 0.f) dH = a.w_curvature * inv_rn * (lap > 0.f ? 1.f : -1.f);
     }
+    if (a.d_hess_ext)  // hessians = [h, h, h] / 3 (modules.py:172-174): d h = sum_c d hess_c / 3
+      dH += ((a.d_hess_ext[3 * slot] + a.d_hess_ext[3 * slot + 1]) + a.d_hess_ext[3 * slot + 2]) / 3.0f;
     float ds[TAPS];
     {
       const float gd = 1.0f / a.grad_den, hh = 0.5f * dH / a.hess_den;

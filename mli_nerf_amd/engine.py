@@ -426,9 +426,12 @@ class RenderEngine:
         return self._aplan[1:]
 
     @torch.no_grad()
-    def backward_a(self, st, d_rgb, flat, grad_flat, grad_table, w_eikonal, w_curvature, progress):
+    def backward_a(self, st, d_rgb, flat, grad_flat, grad_table, w_eikonal, w_curvature, progress,
+                   d_grad_ext=None, d_hess_ext=None):
         """Stage-a gradient of the loss w.r.t. every parameter: the flat buffer (SDF MLP, head,
-        s_var) into grad_flat and the hash table into grad_table (both fully overwritten)."""
+        s_var) into grad_flat and the hash table into grad_table (both fully overwritten).
+        The eikonal / curvature terms are computed in-kernel from their weights (fused path)
+        and/or arrive as d loss / d gradients, hessians ([N][R][3], autograd path)."""
         rays, dists, fld, hd, comp = st
         N, R = dists.shape
         S = N * R
@@ -461,7 +464,7 @@ class RenderEngine:
             L.ptr(fld["grad"]), L.ptr(fld["hess"]), L.ptr(d_sdf), L.ptr(d_grad), L.ptr(d_nrm), L.ptr(dh0),
             L.ptr(fld["enc"]), L.ptr(self.wsdf), L.ptr(self.wsdf_t), self.eps, self.grad_den, self.hess_den,
             float(w_eikonal), float(w_curvature), scale, L.ptr(d_enc), L.ptr(dz0f), L.ptr(b["x0_rows"]),
-            L.ptr(b["dws"][:256]), L.ptr(b["dws"][256:])))
+            L.ptr(b["dws"][:256]), L.ptr(b["dws"][256:]), L.ptr(d_grad_ext), L.ptr(d_hess_ext)))
         grad_table.zero_()
         L.call("mli_hash_bwd", L.HashBwdArgs(R, N, L.ptr(rays["center"]), L.ptr(rays["ray_unit"]), L.ptr(dists),
                                              L.ptr(d_enc), self.levels, self.eps, int(self.active_levels),

@@ -147,29 +147,42 @@ class LumenRGB(torch.nn.Module):
 
 
 class _RenderHeads(torch.autograd.Function):
-    """Forward: the whole stage-b render on the GPU.  Backward: composite -> heads dX chain ->
-    dW GEMMs -> weight-norm backward, producing the gradient of the flat trainable buffer."""
+    """Forward: the whole render on the GPU.  Backward (stage b): composite -> heads dX chain
+    -> dW GEMMs -> weight-norm backward into the flat trainable buffer.  Stage a: the
+    gradients / hessians are differentiable outputs too and the backward runs the geometry
+    chain (Engine.backward_a) into the flat buffer and the hash table."""
 
     @staticmethod
-    def forward(ctx, flat, model, data, u, progress, training):
+    def forward(ctx, flat, table, model, data, u, progress, training):
         eng = model.engine
         st = eng.render(data, model.s_var.detach(), progress, training, u=u, W=model.image_width)
         ctx.state = st
         ctx.model = model
+        ctx.progress = progress
         model._last_state = st
-        comp = st[4]
-        return comp["rgb"], comp["o_r"], comp["o_s"], comp["o_re"]
+        comp, fld = st[4], st[2]
+        if model.stage != "a":
+            return comp["rgb"], comp["o_r"], comp["o_s"], comp["o_re"]
+        hess = fld["hess"].clone() if fld["hess"] is not None else torch.zeros_like(fld["grad"])
+        return comp["rgb"], comp["o_r"], comp["o_s"], comp["o_re"], fld["grad"].clone(), hess
 
     @staticmethod
-    def backward(ctx, d_rgb, d_o_r, d_o_s, d_o_re):
+    def backward(ctx, d_rgb, d_o_r, d_o_s, d_o_re, d_grads=None, d_hess=None):
         model = ctx.model
-        if model.stage == "a":
-            raise NotImplementedError("stage-a gradients (geometry + hash table) run through the fused "
-                                      "Trainer.train_step (mli_nerf_amd.trainer), not torch autograd")
         grad = torch.zeros_like(model.flat)
+        if model.stage == "a":
+            st = ctx.state
+            N, R = st[1].shape
+            d_rgb = torch.zeros(R, 3, device=grad.device) if d_rgb is None else d_rgb.contiguous()
+            gt = torch.empty_like(model.neural_sdf.tcnn_encoding.params)
+            c = lambda t: None if t is None else t.contiguous()  # noqa: E731
+            model.engine.backward_a(st, d_rgb, model.flat.detach(), grad, gt, 0.0, 0.0, ctx.progress,
+                                    d_grad_ext=c(d_grads), d_hess_ext=c(d_hess))
+            ctx.state = None
+            return grad, gt, None, None, None, None, None
         model.engine.backward(ctx.state, d_rgb, d_o_r, d_o_s, d_o_re, model.flat, model._sdf_l1(), grad)
         ctx.state = None
-        return grad, None, None, None, None, None
+        return grad, None, None, None, None, None, None
 
 
 class Model(torch.nn.Module):
@@ -287,8 +300,9 @@ class Model(torch.nn.Module):
         self.prepare()
         u = self.stratified_uniforms(data, u)
         self.image_width = self.image_size_train[1]
-        rgb, o_r, o_s, o_re = _RenderHeads.apply(self.flat, self, data, u, self.progress, self.training)
-        return self.outputs(self._last_state, (rgb, o_r, o_s, o_re))
+        table = self.neural_sdf.tcnn_encoding.params
+        res = _RenderHeads.apply(self.flat, table, self, data, u, self.progress, self.training)
+        return self.outputs(self._last_state, res)
 
     def stratified_uniforms(self, data, u=None):
         """nerf_util.py:33: U[0,1) per coarse bin in training, midpoints (None) in eval."""
@@ -302,14 +316,18 @@ class Model(torch.nn.Module):
         """The reference output dict (NeuralLumen/model.py:312-323) of a render state; ``heads``
         = differentiable (rgb, o_r, o_s, o_re) when called under autograd."""
         rays, dists, fld, hd, comp = st
-        rgb, o_r, o_s, o_re = heads if heads is not None else (comp["rgb"], comp["o_r"], comp["o_s"], comp["o_re"])
+        heads = heads if heads is not None else (comp["rgb"], comp["o_r"], comp["o_s"], comp["o_re"])
+        rgb, o_r, o_s, o_re = heads[:4]
+        grads, hess = (heads[4], heads[5]) if len(heads) == 6 else (fld["grad"], fld["hess"])
+        if len(heads) == 6 and fld["hess"] is None:
+            hess = None
         N, R = dists.shape
         out = dict(rgb=rgb[None], o_r=o_r[None], o_s=o_s[None], o_re=o_re[None],
                    outside=rays["outside"].bool().view(1, R, 1),
                    dists=dists.t().reshape(1, R, N, 1),
                    weights=comp["weights"].t().reshape(1, R, N, 1),
-                   gradients=fld["grad"].permute(1, 0, 2).reshape(1, R, N, 3),
-                   hessians=None if fld["hess"] is None else fld["hess"].permute(1, 0, 2).reshape(1, R, N, 3),
+                   gradients=grads.permute(1, 0, 2).reshape(1, R, N, 3),
+                   hessians=None if hess is None else hess.permute(1, 0, 2).reshape(1, R, N, 3),
                    opacity=None, gradient=None)
         if self.stage == "a":  # mode 'rgb' has no intrinsic outputs (NeuralLumen/model.py:300-303)
             for k in ("o_r", "o_s", "o_re"):

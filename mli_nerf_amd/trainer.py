@@ -310,6 +310,11 @@ class Trainer:
         total.backward()
         grad = reduce_gradients(self.model.flat.grad, self.world_size)
         self.optim.step(grad, self.lr())
+        if self.stage == "a":
+            table = self.model.neural_sdf.tcnn_encoding.params
+            gtab = reduce_gradients(table.grad, self.world_size)
+            self.optim_table.step(gtab, self.lr(), p16=self.model.engine.table16)
+            table.grad = None
         self.current_iteration += 1
         self.losses = {k: v.detach() for k, v in losses.items()}
         self.losses["total"] = total.detach()

@@ -72,12 +72,42 @@ def _corner_index(gx, gy, gz, res, size):
 _CORNER_BITS = torch.tensor([[(c >> d) & 1 for d in range(3)] for c in range(8)], dtype=torch.int64)
 
 
+class _Encode(torch.autograd.Function):
+    """The encoding with an explicit backward w.r.t. the table (tcnn's kernel_grid_backward:
+    every corner receives weight * d output, summed): one dense gradient per call built with
+    index_add_, instead of autograd's per-gather dense zero tensors (which make a stage-a
+    backward over the 1.46 GB table take minutes per step on the CPU)."""
+
+    @staticmethod
+    def forward(ctx, x01, params, table, n_feat):
+        out, cache = _encode_fwd(x01, params, table, n_feat)
+        ctx.cache, ctx.n_params, ctx.n_feat = cache, params.numel(), n_feat
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        grid = torch.zeros(ctx.n_params // ctx.n_feat, ctx.n_feat, dtype=grad_out.dtype)
+        f = ctx.n_feat
+        for lv, (rows, w) in enumerate(ctx.cache):
+            g = grad_out[:, lv * f:(lv + 1) * f]
+            for c in range(8):
+                grid.index_add_(0, rows[:, c], w[c][:, None] * g)
+        ctx.cache = None
+        return None, grid.view(-1), None, None
+
+
 def encode(x01, params, table, n_feat=8):
     """x01 [n,3] float32 in (roughly) [0,1]; params flat float32 -> [n, L*n_feat] float32."""
+    if params.requires_grad and torch.is_grad_enabled():
+        return _Encode.apply(x01, params, table, n_feat)
+    return _encode_fwd(x01, params, table, n_feat)[0]
+
+
+def _encode_fwd(x01, params, table, n_feat):
     x01 = x01.to(torch.float32)
     n = x01.shape[0]
     grid = params.view(-1, n_feat)
-    outs = []
+    outs, cache = [], []
     xd = x01.to(torch.float64)
     for scale, res, size, offset in table:
         # fmaf(scale, x, 0.5): exact product+add in float64, one rounding to float32.
@@ -90,14 +120,17 @@ def encode(x01, params, table, n_feat=8):
         # float weights and the accumulation keep the per-corner order c = 0..7
         gc = (gi[:, None, :] + _CORNER_BITS[None]) & MASK32
         idx8 = _corner_index(gc[..., 0], gc[..., 1], gc[..., 2], res, size)
+        ws = []
         for c in range(8):
             bits = [(c >> d) & 1 for d in range(3)]
             w = torch.ones(n, dtype=torch.float32)
             for d in range(3):
                 w = w * (frac[:, d] if bits[d] else (1.0 - frac[:, d]))
             acc = acc + w[:, None] * grid[offset + idx8[:, c]]
+            ws.append(w)
         outs.append(acc)
-    return torch.cat(outs, dim=-1)
+        cache.append((offset + idx8, ws))
+    return torch.cat(outs, dim=-1), cache
 
 
 class HashGridStub:
