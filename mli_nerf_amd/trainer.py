@@ -138,11 +138,14 @@ class Trainer:
         self.cfg = cfg
         self.model = model
         self.weights = {k: v for k, v in cfg.trainer.loss_weight.items() if v}
-        p = cfg.trainer.para_intrinsic_loss
-        self.ranges = (tuple(p["weight_map_range_shading"]), tuple(p["weight_map_range_visibility"]))
+        # stage-a configs have no intrinsic / residual losses (and no parameters for them)
+        p = cfg.trainer.get("para_intrinsic_loss", None) or {}
+        self.ranges = (tuple(p.get("weight_map_range_shading", (0.0, 1.0))),
+                       tuple(p.get("weight_map_range_visibility", (0.0, 1.0))))
         self.intr_factors = (float(p.get("factor_ref", 1.0)), float(p.get("factor_sha", 1.0)))
-        q = cfg.trainer.para_regularize_re_loss
-        self.re_factors = (q["factor_negative"], q["factor_positive"], q["exponent_positive"])
+        q = cfg.trainer.get("para_regularize_re_loss", None) or {}
+        self.re_factors = (q.get("factor_negative", 10.0), q.get("factor_positive", 1.0),
+                           q.get("exponent_positive", 1.0))
         self._scratch = self._grad = None
         o = cfg.optim
         self.stage = getattr(model, "stage", "b")
