@@ -48,6 +48,7 @@ class PathCfg:
     rgb_mode: str = "rgb_r_s"       # LumenRGB network_mode; "rgb" = stage a (modules.py:50-55)
     active_levels: int = None       # coarse-to-fine mask (modules.py:91-113); None = all levels
     anneal_levels: int = None       # tap epsilon level (modules.py:102-107); None = all levels
+    light_visibility: dict = None   # model.light_visibility when enabled (NeuralLumen/model.py:25-35)
 
     @property
     def n_samples(self):
@@ -358,6 +359,62 @@ def render_rays(weights, cfg, center, ray_unit, pts_light, u=None, training=True
     return out
 
 
+# --------------------------------------------------------------------------------------
+# light visibility for the pseudo labels (NeuralLumen/model.py:133-184, test_all_light)
+# --------------------------------------------------------------------------------------
+def sphere_trace(weights, cfg, center, ray_unit, near, far, iters=20, dist_start=None):
+    """neuralangelo/model.py:298-325 sphere_tracing_intersection (the SDF network's forward:
+    no outside overwrite).  center/ray_unit [B,R,3], near/far/dist_start [B,R,1]."""
+    dist = near.clone() if dist_start is None else dist_start.clone()
+    mask = torch.ones_like(dist, dtype=torch.bool)
+    for _ in range(iters):
+        pts = center + ray_unit * dist
+        sdfs = sdf_net(weights, cfg, pts, with_feat=False)[0]
+        dist[mask] += sdfs[mask]
+        mask[dist > far] = False
+        mask[dist < near] = False
+    dist = torch.clamp(dist, near, far)
+    return dist, center + ray_unit * dist, mask
+
+
+def light_visibility(weights, cfg, vis, center, ray_unit, pts_light, near, far, out):
+    """NeuralLumen/model.py:133-184 get_light_visibility, method 'sphere_tracing' (the one the
+    configs use), camera ray types blend_z_sphere_tracing / blend_z / sphere_tracing; visibility
+    bounds :186-199 (box: the model's bounding_box_aabb, as the reference reads it).
+    ``vis``: dict(camera_ray_type, bounding, radius, aabb, gamma)."""
+    with torch.no_grad():
+        kind = vis["camera_ray_type"]
+        blend = (out["dists"] * out["weights"]).sum(2)                       # render.composite
+        if kind == "blend_z_sphere_tracing":
+            inter_dist, inter_pts, inter_mask = sphere_trace(weights, cfg, center, ray_unit, near, far,
+                                                             dist_start=blend)
+        elif kind == "blend_z":
+            inter_dist = blend
+            inter_pts = center + ray_unit * inter_dist
+            inter_mask = inter_dist > 0.0
+        elif kind == "sphere_tracing":
+            inter_dist, inter_pts, inter_mask = sphere_trace(weights, cfg, center, ray_unit, near, far)
+        else:
+            raise NotImplementedError(kind)
+        light_ray = inter_pts - pts_light
+        light_unit = F.normalize(light_ray, dim=-1)
+        if vis["bounding"] == "box":
+            near_l, far_l, outside_l = aabb_bounds(pts_light, light_unit, vis["aabb"])
+        else:
+            near_l, far_l, outside_l = sphere_bounds(pts_light, light_unit, vis["radius"])
+        far_t = light_ray.norm(dim=-1, keepdim=True) - 1e-3
+        inside = (near_l < far_t) & (far_t < far_l) & ~outside_l
+        _, _, mask_l = sphere_trace(weights, cfg, pts_light, light_unit, near_l, far_t)
+        visibility = (~mask_l) | (~inside)
+        normal = F.normalize(-out["gradient"], dim=-1)
+        nxl = (normal * light_unit).sum(dim=-1, keepdim=True).relu()
+        shading = nxl * visibility.float()
+        if vis.get("gamma"):
+            shading = torch.pow(shading, 1.0 / vis["gamma"])
+    return dict(visibility=visibility, normal_x_light=nxl, pseudo_shading=shading, inter_dist=inter_dist,
+                inter_mask=inter_mask)
+
+
 def forward(weights, cfg, data, u=None, training=True, progress=0.0, width=512, height=None, dists=None):
     """NeuralLumen/model.py:113-131 Model.forward -> render_pixels_lumen."""
     height = height or width
@@ -366,7 +423,16 @@ def forward(weights, cfg, data, u=None, training=True, progress=0.0, width=512, 
     pts_light = light_points(data["pose_light"], height * width)
     bidx = torch.arange(ray.shape[0])[:, None].expand_as(data["ray_idx"])
     pts_light = pts_light[bidx, data["ray_idx"]]
-    return render_rays(weights, cfg, center, ray_unit, pts_light, u, training, progress, dists)
+    out = render_rays(weights, cfg, center, ray_unit, pts_light, u, training, progress, dists)
+    vis = getattr(cfg, "light_visibility", None)
+    if vis and not training:  # NeuralLumen/model.py:325-336 (flag_light_visibility)
+        if cfg.bounding == "box":
+            near, far, _ = aabb_bounds(center, F.normalize(ray, dim=-1), cfg.aabb)
+        else:
+            near, far, _ = sphere_bounds(center, F.normalize(ray, dim=-1))
+        out.update(light_visibility(weights, cfg, vis, center, F.normalize(ray, dim=-1), pts_light, near, far,
+                                    out))
+    return out
 
 
 # --------------------------------------------------------------------------------------

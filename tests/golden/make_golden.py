@@ -47,6 +47,15 @@ STAGE_A_CASES = {
     "hotdog_a_r64_n32_it20k": ("syn_hotdog_a", 64, 16, 4, 4, 14, 3.0, 20000),
     "hotdog_a_r32_n128_it80k": ("syn_hotdog_a", 32, 64, 16, 4, 14, 4.0, 80000),
 }
+# Light visibility (test.py --inference_mode unpairlights_train --model.light_visibility.enabled=True,
+# run_synthetic.sh:13): eval render with the sphere-traced camera / light rays.
+# name -> (config, R, Nc, Nf, H, log2T, light_visibility overrides); s_var 6 (sharp weights) and
+# frame 5 so a sixth of the surface hits are shadowed (visibility not trivially all-true)
+VIS_CASES = {
+    "hotdog_a_vis_r128_n32": ("syn_hotdog_a", 128, 16, 4, 4, 14, {"enabled": True}),
+    "savannah_b_vis_r128_n32": ("rene_savannah_b", 128, 16, 4, 4, 14,
+                                {"enabled": True, "camera_ray_type": "sphere_tracing"}),
+}
 MAX_ITER = 500000      # neuralangelo/configs/base.yaml:13
 WARM_UP_END = 5000     # base.yaml optim.sched.warm_up_end
 
@@ -295,6 +304,60 @@ def run_stage_a_case(name, spec):
     print("wrote %s (%.1f KB)" % (path, os.path.getsize(path) / 1024))
 
 
+def run_vis_case(name, spec):
+    """Eval render of the reference model with light visibility on (the test_all_light
+    inference: every coarse-to-fine level active, NeuralLumen/trainer.py:224-226)."""
+    from projects.nerf.utils import nerf_util, camera
+    from projects.NeuralLumen.model import Model
+    from projects.NeuralLumen.utils.utils import get_center
+    import torch.nn.functional as F
+    config, R, Nc, Nf, H, log2T, vis_over = spec
+    nerf_util.sample_dists.__defaults__ = ("cpu",)
+    cfg = reference_cfg(config, R, Nc, Nf, H, log2T)
+    for k, v in vis_over.items():
+        cfg.model.light_visibility[k] = v
+    H_img, W_img = cfg.data.train.image_size
+    model = Model(cfg.model, cfg.data)
+    stage_a = model.neural_rgb.network_mode == "rgb"
+    sd = synthetic.make_state_dict(log2T=log2T, seed=0, heads="rgb" if stage_a else "rgb_r_s", s_var=6.0)
+    load_weights(model, sd)
+    if hasattr(model, "bounding_box_aabb"):
+        model.bounding_box_aabb = model.bounding_box_aabb.float()
+    model.neural_sdf.warm_up_end = WARM_UP_END
+    if cfg.model.object.sdf.encoding.coarse2fine.enabled:
+        model.neural_sdf.set_active_levels(sys.maxsize)
+    model.neural_sdf.set_normal_epsilon()
+    model.progress = 1.0
+    model.eval()
+    data = synthetic.make_batch(R, H=H_img, W=W_img, frame=5)
+    with torch.no_grad():
+        center, ray = camera.get_center_and_ray(data["pose"], data["intr"], (H_img, W_img))
+        center = nerf_util.slice_by_ray_idx(center, data["ray_idx"])
+        ray = nerf_util.slice_by_ray_idx(ray, data["ray_idx"])
+        pts_light = nerf_util.slice_by_ray_idx(get_center(data["pose_light"], (H_img, W_img)), data["ray_idx"])
+        out = model.render_rays_lumen(center, F.normalize(ray, dim=-1), pts_light, stratified=False)
+    lv = cfg.model.light_visibility
+    fix = dict(R=R, Nc=Nc, Nf=Nf, H=H, log2T=log2T, config=config, H_img=H_img, W_img=W_img, train=False,
+               stage_a=stage_a, s_var=6.0, frame=5, vis=dict(camera_ray_type=lv.get("camera_ray_type"), type=lv.type,
+                                         bounding=lv.visibility_bounding_type,
+                                         radius=float(lv.get("visibility_sphere_radius", 1.0)),
+                                         gamma=float(lv.get("gamma_correlation", 0.0))))
+    for k in ("rgb", "dists", "weights", "gradient", "visibility", "normal_x_light", "pseudo_shading",
+              "inter_dist", "inter_mask", "outside"):
+        fix["out." + k] = out[k].detach().clone()
+    # oracle check
+    pcfg = path_cfg(cfg, Nc, Nf, H, log2T)
+    if stage_a:
+        pcfg.rgb_mode = "rgb"
+    pcfg.light_visibility = dict(fix["vis"], aabb=pcfg.aabb)
+    with torch.no_grad():
+        o_out = o_render.forward(sd, pcfg, data, u=None, training=False, progress=1.0, width=W_img, height=H_img)
+    check(name, fix, o_out, None, None, None)
+    path = os.path.join(HERE, name + ".pt")
+    torch.save(fix, path)
+    print("wrote %s (%.1f KB)" % (path, os.path.getsize(path) / 1024))
+
+
 def main():
     install_stubs()
     only = sys.argv[1:]
@@ -306,6 +369,10 @@ def main():
         if only and name not in only:
             continue
         run_stage_a_case(name, spec)
+    for name, spec in VIS_CASES.items():
+        if only and name not in only:
+            continue
+        run_vis_case(name, spec)
 
 
 if __name__ == "__main__":

@@ -101,3 +101,31 @@ def test_oracle_stage_a_matches_reference_golden(golden, name):
             torch.testing.assert_close(g.flatten()[::97], fx["grad." + name_p + ":strided"], rtol=1e-4, atol=1e-7)
             torch.testing.assert_close(g.double().sum().float(), fx["grad." + name_p + ":sum"],
                                        rtol=1e-4, atol=1e-6)
+
+
+VIS_CASES = ["hotdog_a_vis_r128_n32", "savannah_b_vis_r128_n32"]
+
+
+@pytest.mark.parametrize("name", VIS_CASES)
+def test_oracle_light_visibility_matches_reference_golden(golden, name):
+    """Eval render with light visibility (sphere-traced camera and light rays,
+    NeuralLumen/model.py:133-184): visibility / shading / intersection outputs."""
+    fx = golden(name)
+    cfg = case_cfg(fx)
+    if fx["stage_a"]:
+        cfg.rgb_mode = "rgb"
+    cfg.light_visibility = dict(fx["vis"], aabb=cfg.aabb)
+    sd = synthetic.make_state_dict(log2T=fx["log2T"], seed=0, s_var=fx["s_var"],
+                                   heads="rgb" if fx["stage_a"] else "rgb_r_s")
+    data = synthetic.make_batch(fx["R"], H=fx["H_img"], W=fx["W_img"], frame=fx["frame"])
+    with torch.no_grad():
+        out = o_render.forward(sd, cfg, data, u=None, training=False, progress=1.0, width=fx["W_img"],
+                               height=fx["H_img"])
+    for key, ref in fx.items():
+        if not key.startswith("out."):
+            continue
+        got = out[key[4:]].detach()
+        if ref.dtype == torch.bool:
+            assert torch.equal(got, ref), key
+        else:
+            torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5, msg=key)
