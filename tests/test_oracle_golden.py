@@ -15,7 +15,7 @@ CASES = ["hotdog_r64_n32_full", "hotdog_r64_n128", "hotdog_r64_n32_eval", "pikac
          "savannah_r64_n32_box"]
 
 AABB = {"rene_savannah_b": (-0.66, -0.516, -0.18, 0.66, 0.42, 0.3)}  # rene_savannah_b.yaml:53-60
-WHITE = {"syn_hotdog_b": True, "NRHints_Pikachu_b": False, "rene_savannah_b": False}
+WHITE = {"syn_hotdog_b": True, "NRHints_Pikachu_b": False, "rene_savannah_b": False, "syn_hotdog_a": True}
 
 
 def case_cfg(fx):
