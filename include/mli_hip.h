@@ -186,6 +186,7 @@ typedef struct {
   float* weights;         /* [N][R] */
   float* rgb; float* o_r; float* o_s; float* o_re;   /* [R,3],[R,3],[R],[R,3]             */
   float* opacity; float* gradient; float* depth;     /* [R],[R,3],[R] (NULL to skip)      */
+  float* blend_dist;      /* [R] sum_k w_k d_k (light visibility camera ray start) or NULL   */
 } mli_composite_args;
 int mli_composite_fwd(const mli_composite_args* a, mli_stream_t s);
 
@@ -352,6 +353,30 @@ typedef struct {
   int row0;
 } mli_frag_rows_args;
 int mli_frag_rows(const mli_frag_rows_args* a, mli_stream_t s);
+
+/* ---------------------------------------------------------------- light visibility
+ * Replaces get_light_visibility (NeuralLumen/model.py:133-184, method 'sphere_tracing') with
+ * sphere_tracing_intersection (neuralangelo/model.py:298-325) on the camera ray (camera_ray_type
+ * 0: blend_z_sphere_tracing from the composited depth, 1: blend_z, 2: sphere_tracing from near)
+ * and on the light ray (visibility bounds get_dist_bounds_visibility :186-199), then
+ * visibility = !hit | !inside, normal_x_light = relu(normalize(-gradient) . light_dir),
+ * pseudo_shading = normal_x_light * visibility (^ 1/gamma).  Four launches. */
+typedef struct {
+  int R;
+  const float* center; const float* ray_unit; const float* pts_light;   /* [R,3] */
+  const float* near_; const float* far_;                               /* camera ray bounds [R] */
+  const float* blend_dist;   /* [R] from mli_composite_fwd */
+  const float* gradient;     /* [R,3] composited gradients (eval) */
+  int camera_ray_type, iters;
+  int vis_box;               /* 0: sphere of radius^2 vis_r2, 1: the AABB */
+  float vis_r2; float aabb[6];
+  float gamma;               /* 0: none */
+  const uint16_t* table; mli_grid_levels levels; int active_levels; const void* wsdf;
+  float* light_unit; float* near_l; float* far_t; uint8_t* inside;    /* scratch [R,3],[R],[R],[R] */
+  float* inter_dist; uint8_t* inter_mask; float* inter_pts;           /* [R],[R],[R,3] */
+  uint8_t* visibility; float* normal_x_light; float* pseudo_shading; /* [R] */
+} mli_light_visibility_args;
+int mli_light_visibility(const mli_light_visibility_args* a, mli_stream_t s);
 
 /* ---------------------------------------------------------------- losses
  * Stage-b loss terms and d(total)/d(rgb, o_r, o_s, o_re) in one call (three launches):

@@ -57,7 +57,7 @@ class CompositeArgs(C.Structure):
     _fields_ = [("R", I32), ("N", I32), ("dists", P), ("far_", P), ("ray_unit", P), ("ray_norm", P),
                 ("sdf", P), ("grad", P), ("y", P), ("s_var", P), ("anneal", F32), ("white_bg", I32),
                 ("weights", P), ("rgb", P), ("o_r", P), ("o_s", P), ("o_re", P), ("opacity", P),
-                ("gradient", P), ("depth", P)]
+                ("gradient", P), ("depth", P), ("blend_dist", P)]
 
 
 class CompositeBwdArgs(C.Structure):
@@ -150,6 +150,15 @@ class HashBwdArgs(C.Structure):
                 ("levels", GridLevels), ("eps", F32), ("active_levels", I32), ("d_table", P)]
 
 
+class LightVisibilityArgs(C.Structure):
+    _fields_ = [("R", I32), ("center", P), ("ray_unit", P), ("pts_light", P), ("near_", P), ("far_", P),
+                ("blend_dist", P), ("gradient", P), ("camera_ray_type", I32), ("iters", I32), ("vis_box", I32),
+                ("vis_r2", F32), ("aabb", F32 * 6), ("gamma", F32), ("table", P), ("levels", GridLevels),
+                ("active_levels", I32), ("wsdf", P), ("light_unit", P), ("near_l", P), ("far_t", P),
+                ("inside", P), ("inter_dist", P), ("inter_mask", P), ("inter_pts", P), ("visibility", P),
+                ("normal_x_light", P), ("pseudo_shading", P)]
+
+
 class FragRowsArgs(C.Structure):
     _fields_ = [("src", P), ("tile_stride", I64), ("tiles", I32), ("k_steps", I32), ("order", I32), ("dst", P),
                 ("ld", I64), ("col0", I64), ("row0", I32)]
@@ -166,6 +175,7 @@ ENTRY_POINTS = {
     "mli_adamw": AdamwArgs, "mli_cast_f16": CastArgs, "mli_stage_b_loss": LossArgs,
     "mli_composite_bwd_geo": CompositeBwdGeoArgs, "mli_geo_bwd": GeoBwdArgs, "mli_sdf_bwd": SdfBwdArgs,
     "mli_pack_sdf_t": PackSdfTArgs, "mli_hash_bwd": HashBwdArgs, "mli_frag_rows": FragRowsArgs,
+    "mli_light_visibility": LightVisibilityArgs,
 }
 
 _lib = None

@@ -122,4 +122,34 @@ MLI_FI void block_sync() {
   asm volatile("" ::: "memory");
 }
 
+// Ray bounds: intersect_with_sphere (nerf_util.py:199-205; r2 = fp32(radius**2)) with the
+// NaN-miss dummy (neuralangelo/model.py:426-429), or the AABB slab test
+// (NeuralLumen/utils/utils.py:86-123, neuralangelo/model.py:422-424).
+MLI_FI void ray_bounds(const float (&c)[3], const float (&v)[3], int box, float r2, const float* aabb, float& nr,
+                       float& fr, bool& out) {
+  if (!box) {
+    const float ctc = (c[0] * c[0] + c[1] * c[1]) + c[2] * c[2];
+    const float ctv = (c[0] * v[0] + c[1] * v[1]) + c[2] * v[2];
+    const float disc = ctv * ctv - (ctc - r2);
+    const float sq = sqrtf(disc);
+    const float n0 = -ctv - sq;
+    out = isnan(n0);
+    nr = out ? 1.0f : fmaxf(n0, 0.0f);
+    fr = out ? 1.2f : -ctv + sq;
+  } else {
+    float tmin = -INFINITY, tmax = INFINITY;
+    for (int i = 0; i < 3; ++i) {
+      const float t0 = (aabb[i] - c[i]) / v[i];
+      const float t1 = (aabb[3 + i] - c[i]) / v[i];
+      tmin = fmaxf(tmin, fminf(t0, t1));
+      tmax = fminf(tmax, fmaxf(t0, t1));
+    }
+    tmin = fminf(fmaxf(tmin, 0.0f), 1e10f);
+    tmax = fminf(fmaxf(tmax, 0.0f), 1e10f);
+    out = tmax <= tmin;
+    nr = out ? 1.0f : tmin;
+    fr = out ? 1.2f : tmax;
+  }
+}
+
 #define MLI_LAUNCH_CHECK() return (int)hipGetLastError()

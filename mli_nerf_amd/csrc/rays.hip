@@ -57,29 +57,7 @@ __global__ __launch_bounds__(256) void rays_kernel(mli_rays_args a) {
   a.ray_norm[r] = nrm;
   float nr, fr;
   bool out;
-  if (a.bounding == 0) {  // nerf_util.py:199-205, neuralangelo/model.py:426-429
-    const float ctc = (c[0] * c[0] + c[1] * c[1]) + c[2] * c[2];
-    const float ctv = (c[0] * v[0] + c[1] * v[1]) + c[2] * v[2];
-    const float disc = ctv * ctv - (ctc - 1.0f);
-    const float sq = sqrtf(disc);
-    const float n0 = -ctv - sq;
-    out = isnan(n0);
-    nr = out ? 1.0f : fmaxf(n0, 0.0f);
-    fr = out ? 1.2f : -ctv + sq;
-  } else {  // NeuralLumen/utils/utils.py:86-123
-    float tmin = -INFINITY, tmax = INFINITY;
-    for (int i = 0; i < 3; ++i) {
-      const float t0 = (a.aabb[i] - c[i]) / v[i];
-      const float t1 = (a.aabb[3 + i] - c[i]) / v[i];
-      tmin = fmaxf(tmin, fminf(t0, t1));
-      tmax = fminf(tmax, fmaxf(t0, t1));
-    }
-    tmin = fminf(fmaxf(tmin, 0.0f), 1e10f);
-    tmax = fminf(fmaxf(tmax, 0.0f), 1e10f);
-    out = tmax <= tmin;
-    nr = out ? 1.0f : tmin;
-    fr = out ? 1.2f : tmax;
-  }
+  ray_bounds(c, v, a.bounding, 1.0f, a.aabb, nr, fr, out);
   a.near_[r] = nr;
   a.far_[r] = fr;
   a.outside[r] = out ? 1 : 0;
@@ -364,6 +342,7 @@ __global__ __launch_bounds__(CW * 64) void composite_fwd_kernel(mli_composite_ar
   if (a.opacity) a.opacity[r] = op;
   if (a.gradient) for (int i = 0; i < 3; ++i) a.gradient[3 * r + i] = acc[8 + i];
   if (a.depth) a.depth[r] = acc[11] / a.ray_norm[r];
+  if (a.blend_dist) a.blend_dist[r] = acc[11];  // render.composite(dists, weights)
 }
 
 // Backward of the composite + heads' output sigmoids: one thread per sample (no scan: the

@@ -892,6 +892,113 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a, int 
   }
 }
 
+
+// ================================================================ light visibility
+struct TraceArgs {
+  int R, iters, active;
+  const float* origin; const float* dir;  // [R,3]
+  const float* near_; const float* far_;  // [R]
+  const float* start;                     // [R] or NULL (= near)
+  const uint16_t* table;
+  mli_grid_levels levels;
+  const void* wsdf;
+  float* dist; uint8_t* mask; float* pts;  // outputs ([R], [R], [R,3] or NULL)
+};
+
+// sphere_tracing_intersection (neuralangelo/model.py:298-325): one wave = 32 rays (the lane
+// halves split the hash levels, as sdf_kernel), `iters` SDF evaluations of the moving point;
+// dist += sdf while the ray is live, a ray dies once dist leaves [near, far]; finally
+// dist = clamp(dist, near, far) (torch.clamp: NaN propagates) and pts = o + v dist.
+__global__ __launch_bounds__(256) void trace_kernel(TraceArgs t) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  load_weights(lds, t.wsdf);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int tiles = (t.R + 31) >> 5;
+  for (int tile = blockIdx.x * SDF_WAVES + wave; tile < tiles; tile += gridDim.x * SDF_WAVES) {
+    const int r = tile * 32 + c;
+    const bool valid = r < t.R;
+    const int rr = valid ? r : t.R - 1;
+    const float o0 = t.origin[3 * rr], o1 = t.origin[3 * rr + 1], o2 = t.origin[3 * rr + 2];
+    const float v0 = t.dir[3 * rr], v1 = t.dir[3 * rr + 1], v2 = t.dir[3 * rr + 2];
+    const float nr = t.near_[rr], fr = t.far_[rr];
+    float d = t.start ? t.start[rr] : nr;
+    bool live = true;
+#pragma unroll 1
+    for (int it = 0; it < t.iters; ++it) {
+      const uint8_t* lds_t = lds + opaque_v(0);
+      const float px = __fadd_rn(o0, __fmul_rn(v0, d));
+      const float py = __fadd_rn(o1, __fmul_rn(v1, d));
+      const float pz = __fadd_rn(o2, __fmul_rn(v2, d));
+      const float s = sdf_point(lds_t, t.table, t.levels, t.active, lane, px, py, pz, nullptr);
+      if (live) d = d + s;
+      if (d > fr) live = false;
+      if (d < nr) live = false;
+    }
+    d = d < nr ? nr : (d > fr ? fr : d);
+    if (valid && h == 0) {
+      t.dist[r] = d;
+      t.mask[r] = live ? 1 : 0;
+      if (t.pts) {
+        t.pts[3 * r] = __fadd_rn(o0, __fmul_rn(v0, d));
+        t.pts[3 * r + 1] = __fadd_rn(o1, __fmul_rn(v1, d));
+        t.pts[3 * r + 2] = __fadd_rn(o2, __fmul_rn(v2, d));
+      }
+    }
+  }
+}
+
+// camera_ray_type blend_z: the composited depth is the intersection (model.py:143-146)
+__global__ __launch_bounds__(256) void blend_z_kernel(mli_light_visibility_args a) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= a.R) return;
+  const float d = a.blend_dist[r];
+  a.inter_dist[r] = d;
+  a.inter_mask[r] = d > 0.0f ? 1 : 0;
+  for (int i = 0; i < 3; ++i) a.inter_pts[3 * r + i] = __fadd_rn(a.center[3 * r + i], __fmul_rn(a.ray_unit[3 * r + i], d));
+}
+
+// light ray from the light position to the camera-ray intersection (model.py:149-173)
+__global__ __launch_bounds__(256) void light_prep_kernel(mli_light_visibility_args a) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= a.R) return;
+  float lr[3], c[3], v[3];
+  for (int i = 0; i < 3; ++i) {
+    c[i] = a.pts_light[3 * r + i];
+    lr[i] = a.inter_pts[3 * r + i] - c[i];
+  }
+  const float n = sqrtf((lr[0] * lr[0] + lr[1] * lr[1]) + lr[2] * lr[2]);
+  const float den = fmaxf(n, 1e-12f);  // F.normalize
+  for (int i = 0; i < 3; ++i) {
+    v[i] = lr[i] / den;
+    a.light_unit[3 * r + i] = v[i];
+  }
+  float nl, fl;
+  bool out;
+  ray_bounds(c, v, a.vis_box, a.vis_r2, a.aabb, nl, fl, out);
+  const float ft = n - 1e-3f;
+  a.near_l[r] = nl;
+  a.far_t[r] = ft;
+  a.inside[r] = (nl < ft && ft < fl && !out) ? 1 : 0;
+}
+
+// visibility, normal x light, pseudo shading (model.py:169-184, :330-334)
+__global__ __launch_bounds__(256) void light_finalize_kernel(mli_light_visibility_args a, const uint8_t* hit) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= a.R) return;
+  const bool vis = !hit[r] || !a.inside[r];
+  const float g0 = -a.gradient[3 * r], g1 = -a.gradient[3 * r + 1], g2 = -a.gradient[3 * r + 2];
+  const float gn = fmaxf(sqrtf((g0 * g0 + g1 * g1) + g2 * g2), 1e-12f);
+  const float dot = ((g0 / gn) * a.light_unit[3 * r] + (g1 / gn) * a.light_unit[3 * r + 1]) +
+                    (g2 / gn) * a.light_unit[3 * r + 2];
+  const float nxl = fmaxf(dot, 0.0f);
+  float sh = nxl * (vis ? 1.0f : 0.0f);
+  if (a.gamma != 0.0f) sh = powf(sh, 1.0f / a.gamma);
+  a.visibility[r] = vis ? 1 : 0;
+  a.normal_x_light[r] = nxl;
+  a.pseudo_shading[r] = sh;
+}
+
 }  // namespace
 
 extern "C" int mli_sdf(const mli_sdf_args* a, mli_stream_t s) {
@@ -961,5 +1068,29 @@ extern "C" int mli_hash_bwd(const mli_hash_bwd_args* a, mli_stream_t s) {
 #else
   hipLaunchKernelGGL(hash_bwd_kernel, dim3((S / 32 + 3) / 4), dim3(256), 0, (hipStream_t)s, *a, -1);
 #endif
+  MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_light_visibility(const mli_light_visibility_args* a, mli_stream_t s) {
+  if (a->R <= 0) return 0;
+  if (a->camera_ray_type < 0 || a->camera_ray_type > 2 || a->iters < 0) return (int)hipErrorInvalidValue;
+  const hipStream_t st = (hipStream_t)s;
+  const int rb = (a->R + 255) / 256;
+  int tb = (a->R + 32 * SDF_WAVES - 1) / (32 * SDF_WAVES);
+  if (tb > 2048) tb = 2048;
+  TraceArgs t{a->R, a->iters, a->active_levels, a->center, a->ray_unit, a->near_, a->far_,
+              a->camera_ray_type == 0 ? a->blend_dist : nullptr, a->table, a->levels, a->wsdf,
+              a->inter_dist, a->inter_mask, a->inter_pts};
+  if (a->camera_ray_type == 1)
+    hipLaunchKernelGGL(blend_z_kernel, dim3(rb), dim3(256), 0, st, *a);
+  else
+    hipLaunchKernelGGL(trace_kernel, dim3(tb), dim3(256), LDS_SDF, st, t);
+  hipLaunchKernelGGL(light_prep_kernel, dim3(rb), dim3(256), 0, st, *a);
+  // light ray: from the light position over [near_l, far_t]; its hit flag goes into `visibility`
+  // (scratch until the finalize overwrites it) and its distance into pseudo_shading (scratch)
+  TraceArgs tl{a->R, a->iters, a->active_levels, a->pts_light, a->light_unit, a->near_l, a->far_t, nullptr,
+               a->table, a->levels, a->wsdf, a->pseudo_shading, a->visibility, nullptr};
+  hipLaunchKernelGGL(trace_kernel, dim3(tb), dim3(256), LDS_SDF, st, tl);
+  hipLaunchKernelGGL(light_finalize_kernel, dim3(rb), dim3(256), 0, st, *a, (const uint8_t*)a->visibility);
   MLI_LAUNCH_CHECK();
 }

@@ -28,11 +28,14 @@ class PathConfig:
 
     def __init__(self, n_coarse=64, n_fine=16, n_hier=4, white_bg=True, bounding="sphere",
                  aabb=(-1, -1, -1, 1, 1, 1), outside_val=1000.0, anneal_end=0.1, log2T=22,
-                 levels=16, min_logres=5, max_logres=11):
+                 levels=16, min_logres=5, max_logres=11, light_visibility=None):
         self.n_coarse, self.n_fine, self.n_hier = n_coarse, n_fine, n_hier
         self.white_bg, self.bounding, self.aabb = white_bg, bounding, tuple(float(x) for x in aabb)
         self.outside_val, self.anneal_end = outside_val, anneal_end
         self.log2T, self.levels, self.min_logres, self.max_logres = log2T, levels, min_logres, max_logres
+        # model.light_visibility when enabled (NeuralLumen/model.py:25-35): dict(camera_ray_type,
+        # type, bounding, radius, gamma) -- None: off
+        self.light_visibility = light_visibility
 
     @property
     def n_samples(self):
@@ -266,6 +269,8 @@ class RenderEngine:
             out.update(opacity=torch.empty(R, 1, device=self.device),
                        gradient=torch.empty(R, 3, device=self.device),
                        depth=torch.empty(R, 1, device=self.device))
+            if self.cfg.light_visibility:
+                out["blend_dist"] = torch.empty(R, 1, device=self.device)
         anneal = min(progress / self.cfg.anneal_end, 1.0)
         L.call("mli_composite_fwd", L.CompositeArgs(R, N, L.ptr(dists), L.ptr(rays["far"]), L.ptr(rays["ray_unit"]),
                                                     L.ptr(rays["ray_norm"]), L.ptr(fld["sdf"]), L.ptr(fld["grad"]),
@@ -273,8 +278,39 @@ class RenderEngine:
                                                     1 if self.cfg.white_bg else 0, L.ptr(out["weights"]),
                                                     L.ptr(out["rgb"]), L.ptr(out["o_r"]), L.ptr(out["o_s"]),
                                                     L.ptr(out["o_re"]), L.ptr(out.get("opacity")),
-                                                    L.ptr(out.get("gradient")), L.ptr(out.get("depth"))))
+                                                    L.ptr(out.get("gradient")), L.ptr(out.get("depth")),
+                                                    L.ptr(out.get("blend_dist"))))
         return out
+
+    @torch.no_grad()
+    def light_visibility(self, rays, comp, iters=20):
+        """get_light_visibility (NeuralLumen/model.py:133-184): adds visibility, normal_x_light,
+        pseudo_shading, inter_dist, inter_mask ([R,1]) to the composite dict."""
+        vis = self.cfg.light_visibility
+        if vis.get("type", "sphere_tracing") != "sphere_tracing":
+            raise NotImplementedError("light visibility type %r (only 'sphere_tracing', the configs' choice, "
+                                      "is built)" % vis.get("type"))
+        kind = {"blend_z_sphere_tracing": 0, "blend_z": 1, "sphere_tracing": 2}[vis["camera_ray_type"]]
+        R = rays["center"].shape[0]
+        f = lambda *shape: torch.empty(*shape, device=self.device)  # noqa: E731
+        u8 = lambda n: torch.empty(n, 1, dtype=torch.uint8, device=self.device)  # noqa: E731
+        o = dict(inter_dist=f(R, 1), inter_mask=u8(R), visibility=u8(R), normal_x_light=f(R, 1),
+                 pseudo_shading=f(R, 1))
+        scratch = dict(light_unit=f(R, 3), near_l=f(R), far_t=f(R), inside=u8(R), inter_pts=f(R, 3))
+        box = vis.get("bounding", "sphere") == "box"
+        r2 = float(np.float32(float(vis.get("radius", 1.0)) ** 2))
+        L.call("mli_light_visibility", L.LightVisibilityArgs(
+            R, L.ptr(rays["center"]), L.ptr(rays["ray_unit"]), L.ptr(rays["pts_light"]), L.ptr(rays["near"]),
+            L.ptr(rays["far"]), L.ptr(comp["blend_dist"]), L.ptr(comp["gradient"]), kind, iters, 1 if box else 0,
+            r2, (C.c_float * 6)(*self.cfg.aabb), float(vis.get("gamma") or 0.0), L.ptr(self.table16), self.levels,
+            int(self.active_levels), L.ptr(self.wsdf), L.ptr(scratch["light_unit"]), L.ptr(scratch["near_l"]),
+            L.ptr(scratch["far_t"]), L.ptr(scratch["inside"]), L.ptr(o["inter_dist"]), L.ptr(o["inter_mask"]),
+            L.ptr(scratch["inter_pts"]), L.ptr(o["visibility"]), L.ptr(o["normal_x_light"]),
+            L.ptr(o["pseudo_shading"])))
+        o["visibility"] = o["visibility"].bool()
+        o["inter_mask"] = o["inter_mask"].bool()
+        comp.update(o)
+        return comp
 
     def render(self, data, s_var, progress, training, u=None, W=512):
         rays = self.rays(data["pose"], data["intr"], data["pose_light"], data["ray_idx"], W)
@@ -282,6 +318,8 @@ class RenderEngine:
         fld = self.field(rays, dists, training)
         hd = self.heads(rays, dists, fld, training)
         comp = self.composite(rays, dists, fld, hd, s_var, progress, training)
+        if self.cfg.light_visibility and not training:
+            self.light_visibility(rays, comp)
         return rays, dists, fld, hd, comp
 
     # ------------------------------------------------------------------ backward

@@ -40,7 +40,14 @@ def path_config_from(cfg_model, cfg_data):
     hg = cfg_model.object.sdf.encoding.hashgrid
     box = _cfg_get(cfg_data, "bounding_type", "unit_sphere") == "box"
     inside_out = bool(_cfg_get(cfg_model, "object.sdf.mlp.inside_out", False))
-    return PathConfig(n_coarse=ns.coarse, n_fine=ns.fine, n_hier=cfg_model.render.num_sample_hierarchy,
+    lv = _cfg_get(cfg_model, "light_visibility", None)
+    vis = None
+    if lv is not None and _cfg_get(lv, "enabled", False):  # NeuralLumen/model.py:25-35
+        vis = dict(camera_ray_type=_cfg_get(lv, "camera_ray_type", None), type=_cfg_get(lv, "type", None),
+                   bounding=_cfg_get(lv, "visibility_bounding_type", "sphere"),
+                   radius=float(_cfg_get(lv, "visibility_sphere_radius", 1.0)),
+                   gamma=float(_cfg_get(lv, "gamma_correlation", 0.0) or 0.0))
+    return PathConfig(light_visibility=vis, n_coarse=ns.coarse, n_fine=ns.fine, n_hier=cfg_model.render.num_sample_hierarchy,
                       white_bg=bool(cfg_model.background.white), bounding="box" if box else "sphere",
                       aabb=tuple(_cfg_get(cfg_data, "bounding_box_aabb", (-1, -1, -1, 1, 1, 1))),
                       outside_val=1000.0 * (-1 if inside_out else 1),
@@ -336,6 +343,9 @@ class Model(torch.nn.Module):
             out["opacity"] = comp["opacity"][None]
             out["gradient"] = comp["gradient"][None]
             out["depth"] = comp["depth"][None]
+            if "visibility" in comp:  # NeuralLumen/model.py:325-336
+                for k in ("visibility", "normal_x_light", "pseudo_shading", "inter_dist", "inter_mask"):
+                    out[k] = comp[k][None]
         return out
 
     @torch.no_grad()
@@ -360,6 +370,7 @@ class Model(torch.nn.Module):
         # mli_rgb_fwd takes whole 256-sample workgroups: pad each chunk's ray count so
         # R * N % 256 == 0 (repeating the last pixel), drop the padding afterwards
         N = self.pcfg.n_samples
+        vis = self.pcfg.light_visibility is not None
         step = 256 // math.gcd(N, 256)
         dev = self.flat.device
         parts = []
@@ -369,10 +380,10 @@ class Model(torch.nn.Module):
             ridx = torch.arange(start, start + Rp, device=dev).clamp_(max=start + R - 1)[None]
             d = dict(pose=data["pose"], intr=data["intr"], pose_light=data["pose_light"], ray_idx=ridx)
             st = self.engine.render(d, self.s_var.detach(), self.progress, False, u=None, W=W)
-            parts.append(sh.pack(st[4])[:R])
-        local = torch.cat(parts, 0) if parts else torch.zeros(0, sh.N_CHANNELS, device=dev)
+            parts.append(sh.pack(st[4], vis)[:R])
+        local = torch.cat(parts, 0) if parts else torch.zeros(0, sh.n_channels(vis), device=dev)
         packed = sh.gather_tiles(local, n_pix, world, group) if world > 1 else local
-        out = {k: v.contiguous()[None] for k, v in sh.unpack(packed).items()}
+        out = {k: v.contiguous()[None] for k, v in sh.unpack(packed, vis).items()}
         rot = data["pose"][..., :3, :3]
         normal_cam = -out["gradient"] @ rot.transpose(-1, -2)
 
@@ -382,4 +393,9 @@ class Model(torch.nn.Module):
                    normal_map=full(normal_cam))
         for k in ("o_r", "o_s", "o_re"):
             out[k + "_map"] = full(out[k])
+        if vis:  # NeuralLumen/model.py:78-83
+            for k in ("visibility", "normal_x_light", "pseudo_shading", "inter_dist", "inter_mask"):
+                out[k + "_map"] = full(out[k]).float()
+            out["visibility"] = out["visibility"] > 0.5
+            out["inter_mask"] = out["inter_mask"] > 0.5
         return out

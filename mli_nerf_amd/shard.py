@@ -15,6 +15,17 @@ import torch
 # opacity 1, gradient 3, depth 1
 CHANNELS = (("rgb", 3), ("o_r", 3), ("o_s", 1), ("o_re", 3), ("opacity", 1), ("gradient", 3), ("depth", 1))
 N_CHANNELS = sum(c for _, c in CHANNELS)
+# + light visibility (NeuralLumen/model.py:78-83) when enabled
+VIS_CHANNELS = (("visibility", 1), ("normal_x_light", 1), ("pseudo_shading", 1), ("inter_dist", 1),
+                ("inter_mask", 1))
+
+
+def _channels(vis):
+    return CHANNELS + (VIS_CHANNELS if vis else ())
+
+
+def n_channels(vis=False):
+    return sum(c for _, c in _channels(vis))
 
 
 def shard_range(n, rank, world):
@@ -24,14 +35,14 @@ def shard_range(n, rank, world):
     return lo, min(n, lo + per), per
 
 
-def pack(out):
-    """dict of [R, c] tensors -> [R, N_CHANNELS]."""
-    return torch.cat([out[k].reshape(out[k].shape[0], c) for k, c in CHANNELS], dim=1)
+def pack(out, vis=False):
+    """dict of [R, c] tensors -> [R, n_channels] fp32."""
+    return torch.cat([out[k].reshape(out[k].shape[0], c).float() for k, c in _channels(vis)], dim=1)
 
 
-def unpack(packed):
+def unpack(packed, vis=False):
     res, o = {}, 0
-    for k, c in CHANNELS:
+    for k, c in _channels(vis):
         res[k] = packed[:, o:o + c]
         o += c
     return res
