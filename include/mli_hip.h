@@ -378,6 +378,28 @@ typedef struct {
 } mli_light_visibility_args;
 int mli_light_visibility(const mli_light_visibility_args* a, mli_stream_t s);
 
+/* ---------------------------------------------------------------- on-device ray batch
+ * Replaces the per-sample CPU draw of NeuralLumen/data.py:120-132 / data_blender.py:179-195
+ * (ray_idx = randperm(H*W)[:R], then gathers of the image and the pseudo labels): ray r takes
+ * pixel pi(r) of a seeded bijection pi of [0, n_pixels) (4-round Feistel network with cycle
+ * walking), so the R indices are distinct by construction and drawn in parallel; the
+ * device-resident image / pseudo-label planes are gathered in the same launch. */
+typedef struct {
+  uint64_t seed;
+  int64_t n_pixels;
+  int R;
+  const float* image;     /* [3][n_pixels] (torchvision to_tensor layout) or NULL */
+  const float* ref;       /* [3][n_pixels] pseudo_reflectance or NULL */
+  const float* sha;       /* [n_pixels] pseudo_shading_gamma or NULL */
+  const float* cert;      /* [n_pixels] visibility_certainty or NULL */
+  int64_t* ray_idx;       /* [R] */
+  float* image_sampled;   /* [R,3] */
+  float* ref_sampled;     /* [R,3] */
+  float* sha_sampled;     /* [R] */
+  float* cert_sampled;    /* [R] */
+} mli_ray_batch_args;
+int mli_ray_batch(const mli_ray_batch_args* a, mli_stream_t s);
+
 /* ---------------------------------------------------------------- losses
  * Stage-b loss terms and d(total)/d(rgb, o_r, o_s, o_re) in one call (three launches):
  * replaces NeuralLumen/trainer.py:133-149 (_compute_loss) with eikonal/curvature

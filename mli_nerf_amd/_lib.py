@@ -159,6 +159,12 @@ class LightVisibilityArgs(C.Structure):
                 ("normal_x_light", P), ("pseudo_shading", P)]
 
 
+class RayBatchArgs(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("n_pixels", I64), ("R", I32), ("image", P), ("ref", P), ("sha", P),
+                ("cert", P), ("ray_idx", P), ("image_sampled", P), ("ref_sampled", P), ("sha_sampled", P),
+                ("cert_sampled", P)]
+
+
 class FragRowsArgs(C.Structure):
     _fields_ = [("src", P), ("tile_stride", I64), ("tiles", I32), ("k_steps", I32), ("order", I32), ("dst", P),
                 ("ld", I64), ("col0", I64), ("row0", I32)]
@@ -175,7 +181,7 @@ ENTRY_POINTS = {
     "mli_adamw": AdamwArgs, "mli_cast_f16": CastArgs, "mli_stage_b_loss": LossArgs,
     "mli_composite_bwd_geo": CompositeBwdGeoArgs, "mli_geo_bwd": GeoBwdArgs, "mli_sdf_bwd": SdfBwdArgs,
     "mli_pack_sdf_t": PackSdfTArgs, "mli_hash_bwd": HashBwdArgs, "mli_frag_rows": FragRowsArgs,
-    "mli_light_visibility": LightVisibilityArgs,
+    "mli_light_visibility": LightVisibilityArgs, "mli_ray_batch": RayBatchArgs,
 }
 
 _lib = None

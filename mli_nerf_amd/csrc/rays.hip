@@ -485,6 +485,50 @@ __global__ void svar_grad_kernel(mli_composite_bwd_geo_args a) {
   a.d_s_var[0] = expf(a.s_var[0]) * a.d_inv_s_acc[0];  // inv_s = exp(s_var)
 }
 
+
+// --------------------------------------------------------------------------- ray batch
+MLI_FI uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+
+// Bijection of [0, 2^bits) (balanced-ish Feistel, 4 rounds keyed by the seed).
+MLI_FI uint64_t feistel(uint64_t x, int bits, uint64_t seed) {
+  const int lb = bits >> 1, hb = bits - lb;
+  const uint64_t lmask = (1ull << lb) - 1ull, hmask = (1ull << hb) - 1ull;
+  uint64_t L = x >> lb, Rr = x & lmask;  // L: hb bits, Rr: lb bits
+  for (int k = 0; k < 4; ++k) {
+    // alternate which half is mixed so both widths stay valid
+    const uint32_t f = mix32((uint32_t)Rr ^ mix32((uint32_t)(seed >> (8 * k)) + 0x9e3779b9u * (k + 1)) ^
+                             (uint32_t)(seed >> 32));
+    const uint64_t nL = Rr, nR = (L ^ f) & hmask;
+    // swap roles: after a round the widths swap, so re-split the combined value
+    const uint64_t comb = (nL << hb) | nR;  // lb + hb bits
+    L = comb >> lb;
+    Rr = comb & lmask;
+  }
+  return (L << lb) | Rr;
+}
+
+__global__ __launch_bounds__(256) void ray_batch_kernel(mli_ray_batch_args a) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= a.R) return;
+  int bits = 1;
+  while ((1ll << bits) < a.n_pixels) ++bits;
+  uint64_t x = (uint64_t)r;
+  do {  // cycle walking: the bijection of [0, 2^bits) restricted to [0, n_pixels)
+    x = feistel(x, bits, a.seed);
+  } while (x >= (uint64_t)a.n_pixels);
+  const int64_t p = (int64_t)x, n = a.n_pixels;
+  a.ray_idx[r] = p;
+  if (a.image)
+    for (int c = 0; c < 3; ++c) a.image_sampled[3 * r + c] = a.image[c * n + p];
+  if (a.ref)
+    for (int c = 0; c < 3; ++c) a.ref_sampled[3 * r + c] = a.ref[c * n + p];
+  if (a.sha) a.sha_sampled[r] = a.sha[p];
+  if (a.cert) a.cert_sampled[r] = a.cert[p];
+}
+
 }  // namespace
 
 extern "C" int mli_rays(const mli_rays_args* a, mli_stream_t s) {
@@ -530,5 +574,12 @@ extern "C" int mli_composite_bwd_geo(const mli_composite_bwd_geo_args* a, mli_st
   if (a->N > 256) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(composite_bwd_geo_kernel, dim3((a->R + CW - 1) / CW), dim3(CW * 64), 0, (hipStream_t)s, *a);
   hipLaunchKernelGGL(svar_grad_kernel, dim3(1), dim3(1), 0, (hipStream_t)s, *a);
+  MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_ray_batch(const mli_ray_batch_args* a, mli_stream_t s) {
+  if (a->R <= 0) return 0;
+  if (a->n_pixels < a->R || a->n_pixels > (1ll << 40) || !a->ray_idx) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ray_batch_kernel, dim3((a->R + 255) / 256), dim3(256), 0, (hipStream_t)s, *a);
   MLI_LAUNCH_CHECK();
 }

@@ -26,6 +26,7 @@ STRUCTS = {
     "mli_composite_bwd_geo_args": L.CompositeBwdGeoArgs, "mli_geo_bwd_args": L.GeoBwdArgs,
     "mli_sdf_bwd_args": L.SdfBwdArgs, "mli_pack_sdf_t_args": L.PackSdfTArgs, "mli_hash_bwd_args": L.HashBwdArgs,
     "mli_frag_rows_args": L.FragRowsArgs, "mli_light_visibility_args": L.LightVisibilityArgs,
+    "mli_ray_batch_args": L.RayBatchArgs,
 }
 
 
