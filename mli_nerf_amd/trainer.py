@@ -330,8 +330,11 @@ class Trainer:
         os.makedirs(logdir, exist_ok=True)
         name = "epoch_{:05}_iteration_{:09}_checkpoint.pt".format(self.current_epoch, self.current_iteration)
         sd = {"module." + k: v for k, v in self.model.state_dict().items()}
-        torch.save(dict(model=sd, optim=self.optim.state_dict(), sched={"last_epoch": self.current_iteration},
-                        epoch=self.current_epoch, iteration=self.current_iteration), os.path.join(logdir, name))
+        ck = dict(model=sd, optim=self.optim.state_dict(), sched={"last_epoch": self.current_iteration},
+                  epoch=self.current_epoch, iteration=self.current_iteration)
+        if self.optim_table is not None:  # stage a: the hash table's AdamW moments
+            ck["optim_table"] = self.optim_table.state_dict()
+        torch.save(ck, os.path.join(logdir, name))
         with open(os.path.join(logdir, "latest_checkpoint.txt"), "w") as f:
             f.write(name + "\n")
         return os.path.join(logdir, name)
@@ -345,6 +348,15 @@ class Trainer:
         res = self.model.load_state_dict(model_sd, strict=False)
         if resume and "optim" in sd and "exp_avg" in sd["optim"]:
             self.optim.load_state_dict(sd["optim"])
+            if self.optim_table is not None and "optim_table" in sd:
+                self.optim_table.load_state_dict(sd["optim_table"])
             self.current_iteration = sd.get("iteration", 0)
             self.current_epoch = sd.get("epoch", 0)
         return res
+
+    def test_video(self, dataset, setting1, setting2, output_dir, mode="test",
+                   video_content=("rgb", "gt", "o_r", "o_s"), show_pbar=False):
+        """projects/nerf/trainers/base.py:264-346 (see mli_nerf_amd.video)."""
+        from . import video
+        return video.render_video(self.model, dataset, setting1, setting2, output_dir, trainer=self, mode=mode,
+                                  video_content=video_content, show_pbar=show_pbar)

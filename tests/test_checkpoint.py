@@ -1,0 +1,73 @@
+"""Checkpoint bridge, CPU: the imaginaire file layout
+(``epoch_{:05}_iteration_{:09}_checkpoint.pt`` + ``latest_checkpoint.txt``,
+imaginaire/trainers/base.py:570-607), ``module.``-prefixed keys, a stage-a checkpoint
+warm-starting stage b (NeuralLumen/trainer.py:27-42: strict=False, tcnn flat params carried
+over), and stage-a resume with the hash-table optimizer moments.  The fp16 table shadow the
+GPU gathers is rebuilt from the loaded fp32 params (tests/test_gpu_video.py)."""
+import os
+
+import torch
+
+from mli_nerf_amd import synthetic
+from mli_nerf_amd.configs import preset
+
+
+def _model(stage, seed=0):
+    from mli_nerf_amd.model import Model
+    name = "syn_hotdog_a" if stage == "a" else "syn_hotdog_b"
+    cfg = preset(name, rays=32, n_coarse=16, n_fine=4, log2T=12)
+    m = Model(cfg.model, cfg.data)
+    m.load_state_dict(synthetic.make_state_dict(log2T=12, s_var=3.0 + seed, heads="rgb" if stage == "a" else "rgb_r_s",
+                                                seed=seed))
+    return cfg, m
+
+
+def test_checkpoint_layout_and_round_trip(tmp_path):
+    from mli_nerf_amd.trainer import Trainer
+    cfg, m = _model("b")
+    tr = Trainer(cfg, m)
+    tr.current_iteration, tr.current_epoch = 1234, 5
+    tr.optim.m.uniform_()
+    path = tr.save_checkpoint(str(tmp_path))
+    assert os.path.basename(path) == "epoch_00005_iteration_000001234_checkpoint.pt"
+    assert (tmp_path / "latest_checkpoint.txt").read_text().strip() == os.path.basename(path)
+    ck = torch.load(path, weights_only=True)
+    assert all(k.startswith("module.") for k in ck["model"])
+    assert "module.neural_sdf.tcnn_encoding.params" in ck["model"]
+    cfg2, m2 = _model("b", seed=1)
+    tr2 = Trainer(cfg2, m2)
+    tr2.load_checkpoint(str(tmp_path / "latest_checkpoint.txt"))
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, m2.state_dict()[k]), k
+    assert torch.equal(tr2.optim.m, tr.optim.m) and tr2.current_iteration == 1234 and tr2.current_epoch == 5
+
+
+def test_stage_a_checkpoint_warm_starts_stage_b(tmp_path):
+    from mli_nerf_amd.trainer import Trainer
+    cfg_a, ma = _model("a", seed=2)
+    tra = Trainer(cfg_a, ma)
+    tra.optim_table.v.uniform_()
+    tra.current_iteration = 500000
+    path = tra.save_checkpoint(str(tmp_path / "a"))
+    # resume stage a: table moments come back
+    cfg_a2, ma2 = _model("a", seed=3)
+    tra2 = Trainer(cfg_a2, ma2)
+    tra2.load_checkpoint(path)
+    assert torch.equal(tra2.optim_table.v, tra.optim_table.v)
+    # warm start stage b (no resume): SDF, table and s_var from stage a; heads stay
+    cfg_b, mb = _model("b", seed=4)
+    heads_before = {k: v.clone() for k, v in mb.state_dict().items() if k.startswith("neural_rgb")}
+    trb = Trainer(cfg_b, mb)
+    res = trb.load_checkpoint(path, resume=False)
+    sa, sb = ma.state_dict(), mb.state_dict()
+    for k in ("neural_sdf.tcnn_encoding.params", "neural_sdf.mlp.linears.0.weight_v", "neural_sdf.mlp.linear_sdf.bias",
+              "s_var"):
+        assert torch.equal(sa[k], sb[k]), k
+    assert trb.current_iteration == 0
+    # the stage-a single head ('neural_rgb.mlp') has the stage-b key names of its first head
+    for k, v in heads_before.items():
+        if k in sa and sa[k].shape == v.shape:
+            assert torch.equal(sb[k], sa[k]), k
+        else:
+            assert torch.equal(sb[k], v), k
+    assert not res.unexpected_keys or all(k.startswith("neural_rgb") for k in res.unexpected_keys)
