@@ -135,9 +135,13 @@ def run_infer(args, world, rank, dev):
     from mli_nerf_amd.configs import preset
     from mli_nerf_amd.model import Model
     size = args.size
-    cfg = preset(args.config, n_fine=args.fine,
-                 overrides={"data": {"train": {"image_size": [size, size]}, "val": {"image_size": [size, size]}},
-                            "model": {"render": {"rand_rays_val": args.chunk}}})
+    over = {"data": {"train": {"image_size": [size, size]}, "val": {"image_size": [size, size]}},
+            "model": {"render": {"rand_rays_val": args.chunk}}}
+    if args.vis:  # the pseudo-label inference (test.py with light_visibility, syn_hotdog_b.yaml:73-78)
+        over["model"]["light_visibility"] = {"enabled": True, "camera_ray_type": "blend_z_sphere_tracing",
+                                             "type": "sphere_tracing", "visibility_bounding_type": "sphere",
+                                             "visibility_sphere_radius": 0.95}
+    cfg = preset(args.config, n_fine=args.fine, overrides=over)
     model = Model(cfg.model, cfg.data)
     model.load_state_dict(synthetic.make_state_dict(log2T=22, seed=0))
     model = model.to(dev)
@@ -176,7 +180,8 @@ def run_infer(args, world, rank, dev):
     R_chunk = min(args.chunk, -(-n_pix // world))
     ktab, roof = kernel_table(prof, args.frames, R_chunk, N, args.fine, per_launch=True)
     result = {
-        "metric": "rays/sec, syn_hotdog_b video_train inference %dx%d full frame (configs[4])" % (size, size),
+        "metric": "rays/sec, syn_hotdog_b video_train inference %dx%d full frame (configs[4])%s" % (
+            size, size, " + light visibility" if args.vis else ""),
         "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": args.frames,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.frames * 1e3, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f16 MFMA (fp32 accumulate) / fp32",
@@ -302,6 +307,7 @@ def main():
     ap.add_argument("--mode", choices=("train", "infer"), default="train",
                     help="train: BASELINE configs[1] step; infer: configs[4] full-frame render")
     ap.add_argument("--frames", type=int, default=4, help="infer: frames timed (after --warmup frames)")
+    ap.add_argument("--vis", action="store_true", help="infer: light visibility on (sphere-traced camera/light rays)")
     ap.add_argument("--size", type=int, default=800, help="infer: frame is size x size")
     ap.add_argument("--chunk", type=int, default=20000, help="infer: rand_rays_val")
     ap.add_argument("--iteration", type=int, default=100000,
@@ -336,8 +342,24 @@ def main():
         # steady state of stage a: past the coarse-to-fine ramp (all 16 levels active)
         trainer.current_iteration = args.iteration
     Hh, W = cfg.data.train.image_size
-    batch = {k: v.to(dev) for k, v in synthetic.make_batch(args.rays, H=Hh, W=W, frame=rank).items()}
     R, N = args.rays, model.pcfg.n_samples
+    # training frames resident in HBM; every step draws its R rays on the device
+    # (mli_ray_batch: distinct pixels + image / pseudo-label gather) inside the timed region
+    from mli_nerf_amd.data import DeviceFeed
+    n_frames = 8
+    g = torch.Generator().manual_seed(1000 + rank)
+    cams = []
+    for f in range(n_frames):
+        fb = synthetic.make_batch(1, H=Hh, W=W, frame=rank * n_frames + f)
+        cams.append((fb["intr"][0], fb["pose"][0], fb["pose_light"][0]))
+    feed = DeviceFeed(device=dev, images=torch.rand(n_frames, 3, Hh * W, generator=g),
+                      pseudo=(torch.rand(n_frames, 3, Hh * W, generator=g), torch.rand(n_frames, Hh * W, generator=g),
+                              torch.rand(n_frames, Hh * W, generator=g)), cameras=cams)
+    draws = iter(range(1 << 62))
+
+    def next_batch():
+        i = next(draws)
+        return feed.batch(i % n_frames, (rank << 40) + i, R)
 
     def barrier():
         if world > 1:
@@ -345,7 +367,7 @@ def main():
             dist.barrier()
 
     for _ in range(args.warmup):
-        trainer.train_step(batch)
+        trainer.train_step(next_batch())
     torch.cuda.synchronize()
     progress("warm-up done (%d steps)" % args.warmup)
     barrier()
@@ -354,7 +376,7 @@ def main():
         L.PROFILE = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        trainer.train_step(batch)
+        trainer.train_step(next_batch())
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()

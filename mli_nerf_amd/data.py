@@ -336,7 +336,9 @@ class DeviceFeed:
             if (self.ref.shape != self.images.shape or self.sha.shape != self.images.shape[::2]
                     or self.cert.shape != self.sha.shape):
                 raise ValueError("pseudo labels must be [F,3,H*W], [F,H*W], [F,H*W]")
-        self.cameras = cameras
+        # cameras resident on the device too: a step makes no host -> device copy
+        self.cameras = None if cameras is None else [
+            tuple(torch.as_tensor(c).float().to(self.device)[None] for c in cam) for cam in cameras]
 
     def __len__(self):
         return self.images.shape[0]
@@ -368,8 +370,7 @@ class DeviceFeed:
         d = dict(idx=torch.tensor([idx]), ray_idx=ray_idx[None], image_sampled=img_s[None])
         if self.cameras is not None:
             intr, pose, light = self.cameras[idx]
-            d.update(intr=intr[None].to(self.device), pose=pose[None].to(self.device),
-                     pose_light=light[None].to(self.device))
+            d.update(intr=intr, pose=pose, pose_light=light)
         if ref_s is not None:
             d.update(pseudo_ref_sampled=ref_s[None], pseudo_sha_sampled=sha_s[None, :, None],
                      pseudo_visibility_certainty_sampled=cert_s[None, :, None])
