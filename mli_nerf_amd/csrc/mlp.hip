@@ -31,7 +31,7 @@ constexpr int FRAG_TILE = 16 * 64 * 8;  // halves per 32-sample tile of a 256-wi
 // weight ring: NSLOT slots of 3 x 8 KiB (one 16 B LDS-DMA per thread per 8 KiB round)
 constexpr int GLDS = 3;
 constexpr int SLOT = GLDS * 8192;       // >= CH(19) = 19584
-constexpr int DIST = 2;                 // chunks in flight ahead of the one being read
+constexpr int DIST = 2;                 // chunks in flight ahead of the one being read (3: no gain)
 constexpr int NSLOT = DIST + 1;
 // feature-major staging ([32 features][256 samples] fp16 per n-tile), double buffered
 constexpr int SROW = 256 * 2 + 16;      // 16 B pad

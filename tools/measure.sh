@@ -29,3 +29,9 @@ fi
 if [ "$WHAT" = infer ] || [ "$WHAT" = all ]; then
   run bench_infer 400 --mode infer --frames 3 --warmup 1 || exit 1
 fi
+if [ "$WHAT" = vis ] || [ "$WHAT" = all ]; then
+  run bench_infer_vis 400 --mode infer --vis --frames 3 --warmup 1 --no-cpu || exit 1
+fi
+if [ "$WHAT" = pikachu ] || [ "$WHAT" = all ]; then
+  run bench_pikachu 300 --config NRHints_Pikachu_b --rays 8192 --fine 32 --no-cpu || exit 1
+fi
