@@ -120,12 +120,13 @@ MLI_FI void stage_flush(Stager& sg, const uint8_t* lds, int S) {
   sg.pend = nullptr;
 }
 
-// ReLU as one v_max_f32 (fmaxf on an MFMA result adds a canonicalising v_max first:
-// measured 4 % of the heads forward)
+// ReLU as one v_max_i32 on the bit pattern: fmaxf on an MFMA result adds a canonicalising
+// v_max first (measured 4 % of the heads forward). Every negative float (and -0) has the sign
+// bit set, so max(bits, 0) is ReLU. Plain C++, not inline asm: the compiler must see the read
+// of the MFMA result to insert the MFMA -> VALU wait states (an asm v_max_f32 read the
+// accumulator before the MFMA had written it back).
 MLI_FI float relu1(float x) {
-  float r;
-  asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(x));
-  return r;
+  return __builtin_bit_cast(float, max(__builtin_bit_cast(int, x), 0));
 }
 // acc = W_chunk (32 x 16*KS) * X (16*KS x 32) + bias
 template <int KS>
