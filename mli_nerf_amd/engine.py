@@ -78,7 +78,8 @@ class RenderEngine:
         self._kmaps = []  # keep host kmap tensors alive
         self.tlayout, self.n_train = layout.trainable_layout(stage)
         self.toff = {name: (off, shape) for name, shape, off in self.tlayout}
-        self._bufs = {}
+        self._lanes = {0: {}}
+        self._bufs = self._lanes[0]  # the current lane's scratch buffers (see use_lane)
         self.u_fine = (C.c_float * 64)(*(layout.u_fine(cfg.n_fine) + [2.0] * (64 - cfg.n_fine)))
         self._pack_descs = None
         self.trace = None  # set to a list to record per-round sampler outputs (debug/tests)
@@ -152,6 +153,12 @@ class RenderEngine:
         return flat[off:off + n].reshape(shape)
 
     # ------------------------------------------------------------------ buffers
+    def use_lane(self, lane):
+        """Switch to scratch-buffer set ``lane``: renders in flight on different streams (the
+        pipelined inference chunks, Model.inference) each own a buffer set; a lane is reused
+        only on its own stream, so stream order protects it."""
+        self._bufs = self._lanes.setdefault(lane, {})
+
     def _buf(self, name, shape, dtype=torch.float32):
         t = self._bufs.get(name)
         n = int(np.prod(shape))

@@ -231,6 +231,7 @@ class Model(torch.nn.Module):
         if self.pcfg.bounding == "box":
             self.bounding_box_aabb = torch.tensor(self.pcfg.aabb)
         self.engine = None
+        self._streams = None  # inference chunk-pipeline streams
         self._sdf_version = None
         self.image_width = self.image_size_train[1]
 
@@ -374,13 +375,29 @@ class Model(torch.nn.Module):
         step = 256 // math.gcd(N, 256)
         dev = self.flat.device
         parts = []
-        for start in range(lo, hi, self.rand_rays_val):
-            R = min(self.rand_rays_val, hi - start)
-            Rp = -(-R // step) * step
-            ridx = torch.arange(start, start + Rp, device=dev).clamp_(max=start + R - 1)[None]
-            d = dict(pose=data["pose"], intr=data["intr"], pose_light=data["pose_light"], ray_idx=ridx)
-            st = self.engine.render(d, self.s_var.detach(), self.progress, False, u=None, W=W)
-            parts.append(sh.pack(st[4], vis)[:R])
+        # Two chunks in flight on two streams, each with its own engine buffer lane: one
+        # chunk's gather-bound sampling / FIELD kernels overlap the other's MFMA-bound heads.
+        main = torch.cuda.current_stream(dev)
+        if self._streams is None or self._streams[0].device != dev:
+            self._streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+        for s in self._streams:
+            s.wait_stream(main)
+        try:
+            for i, start in enumerate(range(lo, hi, self.rand_rays_val)):
+                R = min(self.rand_rays_val, hi - start)
+                Rp = -(-R // step) * step
+                with torch.cuda.stream(self._streams[i % 2]):
+                    self.engine.use_lane(i % 2)
+                    ridx = torch.arange(start, start + Rp, device=dev).clamp_(max=start + R - 1)[None]
+                    d = dict(pose=data["pose"], intr=data["intr"], pose_light=data["pose_light"], ray_idx=ridx)
+                    st = self.engine.render(d, self.s_var.detach(), self.progress, False, u=None, W=W)
+                    parts.append(sh.pack(st[4], vis)[:R])
+        finally:
+            self.engine.use_lane(0)
+            for s in self._streams:
+                main.wait_stream(s)
+        for p in parts:
+            p.record_stream(main)
         local = torch.cat(parts, 0) if parts else torch.zeros(0, sh.n_channels(vis), device=dev)
         packed = sh.gather_tiles(local, n_pix, world, group) if world > 1 else local
         out = {k: v.contiguous()[None] for k, v in sh.unpack(packed, vis).items()}
