@@ -159,8 +159,6 @@ def run_infer(args, world, rank, dev):
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    if not args.no_kernel_timing:
-        L.PROFILE = []
     t0 = time.perf_counter()
     out = None
     for f in range(args.warmup, args.warmup + args.frames):
@@ -169,6 +167,15 @@ def run_infer(args, world, rank, dev):
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # per-kernel HIP events over one more (untimed) frame rendered with the chunk pipeline off:
+    # with two chunks in flight an event pair would also time the other stream's kernels
+    n_prof = 0 if args.no_kernel_timing else 1
+    if n_prof:
+        model.pipeline_chunks = False
+        L.PROFILE = []
+        model.inference(frames[-1])
+        torch.cuda.synchronize()
+        model.pipeline_chunks = True
     prof, L.PROFILE = L.PROFILE, None
     if world > 1:
         import torch.distributed as dist
@@ -178,7 +185,7 @@ def run_infer(args, world, rank, dev):
     n_pix = size * size
     value = n_pix * args.frames / elapsed
     R_chunk = min(args.chunk, -(-n_pix // world))
-    ktab, roof = kernel_table(prof, args.frames, R_chunk, N, args.fine, per_launch=True)
+    ktab, roof = kernel_table(prof, max(n_prof, 1), R_chunk, N, args.fine, per_launch=True)
     result = {
         "metric": "rays/sec, syn_hotdog_b video_train inference %dx%d full frame (configs[4])%s" % (
             size, size, " + light visibility" if args.vis else ""),
@@ -373,7 +380,7 @@ def main():
     barrier()
     torch.cuda.synchronize()
     if not args.no_kernel_timing:
-        L.PROFILE = []
+        L.PROFILE = []  # per-kernel HIP events on the launch stream, over the timed region
     t0 = time.perf_counter()
     for _ in range(args.steps):
         trainer.train_step(next_batch())

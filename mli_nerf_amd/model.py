@@ -232,6 +232,7 @@ class Model(torch.nn.Module):
             self.bounding_box_aabb = torch.tensor(self.pcfg.aabb)
         self.engine = None
         self._streams = None  # inference chunk-pipeline streams
+        self.pipeline_chunks = True  # two inference chunks in flight (False: one stream)
         self._sdf_version = None
         self.image_width = self.image_size_train[1]
 
@@ -386,8 +387,9 @@ class Model(torch.nn.Module):
             for i, start in enumerate(range(lo, hi, self.rand_rays_val)):
                 R = min(self.rand_rays_val, hi - start)
                 Rp = -(-R // step) * step
-                with torch.cuda.stream(self._streams[i % 2]):
-                    self.engine.use_lane(i % 2)
+                lane = i % 2 if self.pipeline_chunks else 0
+                with torch.cuda.stream(self._streams[lane]):
+                    self.engine.use_lane(lane)
                     ridx = torch.arange(start, start + Rp, device=dev).clamp_(max=start + R - 1)[None]
                     d = dict(pose=data["pose"], intr=data["intr"], pose_light=data["pose_light"], ray_idx=ridx)
                     st = self.engine.render(d, self.s_var.detach(), self.progress, False, u=None, W=W)

@@ -274,6 +274,28 @@ def test_inference_full_image():
     torch.testing.assert_close(out["rgb_map"][0].permute(1, 2, 0).reshape(-1, 3), out["rgb"][0])
 
 
+def test_inference_chunking_invariant():
+    """The pipelined inference (chunks alternate between two streams, each with its own
+    engine buffer lane) against a one-chunk render of the same frame: every ray is computed
+    independently of its chunk, so the maps must be bit-identical.  Ragged: 432 pixels in
+    chunks of 97 (5 chunks, the last one 44 rays, padded to whole workgroups), so both lanes
+    are reused."""
+    _need_gpu()
+    model, sd, data, pcfg, (Hh, W) = build("syn_hotdog_b", 64, 16, 4, 4, 14, 3.0)
+    model.image_size_val = [18, 24]
+    d = to_dev(data)
+    model.rand_rays_val = 97
+    chunked = model.inference(d)
+    chunked2 = model.inference(d)  # second call reuses the streams and the lane buffers
+    model.rand_rays_val = 4096
+    whole = model.inference(d)
+    torch.cuda.synchronize()
+    for key in ("rgb", "o_r", "o_s", "o_re", "opacity", "gradient", "depth"):
+        diff = (chunked[key] - whole[key]).abs().max().item()
+        assert torch.equal(chunked[key], whole[key]), (key, diff)
+        assert torch.equal(chunked2[key], whole[key]), key
+
+
 @pytest.mark.parametrize("case", ["hotdog", "pikachu"])
 def test_fused_loss_step_matches_autograd_step(case):
     """Trainer hot path (mli_stage_b_loss: loss terms + d/d outputs in HIP, no autograd)

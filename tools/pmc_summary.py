@@ -26,8 +26,8 @@ def short(name):
     """Kernel symbol -> the C-ABI call bench.py times (kernel table names)."""
     table = [("rgb_fwd_kernel", "mli_rgb_fwd"), ("rgb_bwd_kernel", "mli_rgb_bwd"),
              ("wgrad_kernel<256, 256", "mli_wgrad:big"), ("wgrad_kernel<256, 320", "mli_wgrad:wide"),
-             ("wgrad_kernel<32, 256", "mli_wgrad:thin"), ("sdf_kernel<1>", "mli_sdf:field"),
-             ("sdf_kernel<0>", "mli_sdf:sdf"), ("sample_fine_kernel", "mli_sample_fine"),
+             ("wgrad_kernel<32, 256", "mli_wgrad:thin"), ("encode5_kernel", "mli_sdf:field/encode5"),
+             ("field_mlp_kernel", "mli_sdf:field/mlp"), ("sdf_kernel", "mli_sdf:sdf"), ("sample_fine_kernel", "mli_sample_fine"),
              ("composite_fwd_kernel", "mli_composite_fwd"), ("composite_bwd_kernel", "mli_composite_bwd"),
              ("adamw_kernel", "mli_adamw"), ("pack_kernel", "mli_pack")]
     for key, val in table:
