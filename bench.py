@@ -191,7 +191,8 @@ def run_infer(args, world, rank, dev):
             size, size, " + light visibility" if args.vis else ""),
         "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": args.frames,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.frames * 1e3, 3), "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "f16 MFMA (fp32 accumulate) / fp32",
+        "scaling": "strong", "vs_baseline": None, "dtype": "fp16",
+        "dtype_detail": "fp16 MFMA operands, fp32 accumulate; fp32 sampling / compositing / losses / AdamW",
         "data": "synthetic (seeded cameras/lights, random-init weights, full 2^22 hash table)",
         "config": {"workload": "%s inference, %dx%d frames, %d-ray chunks, tile-sharded" % (args.config, size, size,
                                                                                             args.chunk),
@@ -406,7 +407,8 @@ def main():
         "metric": "rays/sec + PSNR, syn_hotdog 4096 rays x128 samples, 1/2/4/8 MI355X",
         "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f16 MFMA (fp32 accumulate) / fp32",
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp16",
+        "dtype_detail": "fp16 MFMA operands, fp32 accumulate; fp32 sampling / compositing / losses / AdamW",
         "data": "synthetic (seeded cameras/lights/labels, random-init weights, full 2^22 hash table)",
         "config": {"workload": "%s stage-%s train step" % (args.config, model.stage), "rays_per_gpu": R,
                    "samples_per_ray": N, "global_rays": R * world, "image": [Hh, W], "parallelism": "dp%d" % world},
