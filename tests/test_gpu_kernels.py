@@ -74,3 +74,25 @@ def test_wgrad_wide_jobs_sharing_b(S):
         err_b = ((db - rb).abs().max() / rb.abs().max()).item()
         print("wide job %d: rel err dW %.2e db %.2e" % (i, err_w, err_b))
         assert err_w < 1e-4 and err_b < 1e-4
+
+
+def test_abi_rejects_bad_shapes_and_accepts_empty():
+    """Error convention of the C ABI (include/mli_hip.h): shapes a kernel's grid cannot take
+    are refused before any launch (non-zero hipError_t -> RuntimeError on the Python side,
+    no CPU fallback), and an empty batch is a no-op that returns 0."""
+    _need_gpu()
+    from mli_nerf_amd import _lib as L
+    from mli_nerf_amd.engine import _grid_levels, PathConfig
+    # heads forward: R * N must be whole 256-sample workgroups; 1 or 3 heads
+    with pytest.raises(RuntimeError, match="mli_rgb_fwd"):
+        L.call("mli_rgb_fwd", L.RgbFwdArgs(3, 32, *([None] * 12), 3))
+    with pytest.raises(RuntimeError, match="mli_rgb_fwd"):
+        L.call("mli_rgb_fwd", L.RgbFwdArgs(8, 32, *([None] * 12), 2))
+    # weight gradients: the sample count must be whole 64-sample k-steps
+    with pytest.raises(RuntimeError, match="mli_wgrad"):
+        L.call("mli_wgrad", L.WgradArgs(100, 0, None, 7))
+    # SDF on an empty batch: nothing to launch, success
+    levels, _ = _grid_levels(PathConfig(log2T=14))
+    L.call("mli_sdf", L.SdfArgs(0, 0, 32, None, None, None, None, None, levels, None, 0.0, 1.0, 1.0,
+                                1000.0, 0, None, None, None, None, None, 16))
+    torch.cuda.synchronize()
