@@ -312,6 +312,12 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--time-all-kernels", action="store_true",
+                    help="train: HIP events around every launch (default: the MFMA kernels only; "
+                         "each event pair costs GPU time between launches)")
+    ap.add_argument("--pipeline", choices=("off", "call", "heads", "wgrad"), default="off",
+                    help="train: prefetch the next batch's geometry (sampling/FIELD) on a side stream, "
+                         "gated as Trainer.prefetch_gate; measured 13 %% slower than off (DESIGN §9)")
     ap.add_argument("--mode", choices=("train", "infer"), default="train",
                     help="train: BASELINE configs[1] step; infer: configs[4] full-frame render")
     ap.add_argument("--frames", type=int, default=4, help="infer: frames timed (after --warmup frames)")
@@ -374,17 +380,38 @@ def main():
             import torch.distributed as dist
             dist.barrier()
 
+    # --pipeline: step k draws batch k+1 and issues its geometry (rays, sampling rounds, FIELD:
+    # frozen SDF) on a side stream (Trainer.prefetch), and trains on batch k.  Every timed step
+    # still draws, samples, renders and trains one full batch.  Off by default: slower.
+    pipe = args.pipeline != "off" and model.stage == "b"
+    cur = next_batch()
+    if pipe:
+        trainer.prefetch(cur)
+
+    trainer.prefetch_gate = args.pipeline if pipe else "call"
+
+    def step():
+        nonlocal cur
+        nxt = next_batch()
+        if pipe and args.pipeline == "call":
+            trainer.prefetch(nxt)
+        trainer.train_step(cur)
+        if pipe and args.pipeline != "call":
+            trainer.prefetch(nxt)
+        cur = nxt
+
     for _ in range(args.warmup):
-        trainer.train_step(next_batch())
+        step()
     torch.cuda.synchronize()
     progress("warm-up done (%d steps)" % args.warmup)
     barrier()
     torch.cuda.synchronize()
     if not args.no_kernel_timing:
         L.PROFILE = []  # per-kernel HIP events on the launch stream, over the timed region
+        L.PROFILE_NAMES = None if args.time_all_kernels else {"mli_rgb_fwd", "mli_rgb_bwd", "mli_wgrad", "mli_sdf"}
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        trainer.train_step(next_batch())
+        step()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -411,7 +438,8 @@ def main():
         "dtype_detail": "fp16 MFMA operands, fp32 accumulate; fp32 sampling / compositing / losses / AdamW",
         "data": "synthetic (seeded cameras/lights/labels, random-init weights, full 2^22 hash table)",
         "config": {"workload": "%s stage-%s train step" % (args.config, model.stage), "rays_per_gpu": R,
-                   "samples_per_ray": N, "global_rays": R * world, "image": [Hh, W], "parallelism": "dp%d" % world},
+                   "samples_per_ray": N, "global_rays": R * world, "image": [Hh, W], "parallelism": "dp%d" % world,
+                   "pipeline": ("geometry prefetch on a side stream, gate " + args.pipeline) if pipe else "off"},
         "psnr": round(psnr, 4), "loss": round(loss, 6),
         "roofline": roof, "kernels": ktab,
         "mfma_tflops_step": round(sum(kernel_flops(n, R, N, 64, args.fine, 4, model.stage) for n in ktab) /

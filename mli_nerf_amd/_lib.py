@@ -222,13 +222,14 @@ def ptr(t):
 # Optional per-launch timing: set to a list to record (name, start_event, end_event) for every
 # C-ABI call on the current stream (used by bench.py for the live roofline measurement).
 PROFILE = None
+PROFILE_NAMES = None  # with PROFILE on: the call names to time (None = every call)
 
 
 def call(name, args, stream=None):
     import torch
     if stream is None:
         stream = torch.cuda.current_stream().cuda_stream
-    if PROFILE is not None:
+    if PROFILE is not None and (PROFILE_NAMES is None or name in PROFILE_NAMES):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         rc = getattr(lib(), name)(C.byref(args), stream)

@@ -80,6 +80,7 @@ class RenderEngine:
         self.toff = {name: (off, shape) for name, shape, off in self.tlayout}
         self._lanes = {0: {}}
         self._bufs = self._lanes[0]  # the current lane's scratch buffers (see use_lane)
+        self.gate_wgrad, self.gate_event = False, None  # event before the dW launches (Trainer.prefetch)
         self.u_fine = (C.c_float * 64)(*(layout.u_fine(cfg.n_fine) + [2.0] * (64 - cfg.n_fine)))
         self._pack_descs = None
         self.trace = None  # set to a list to record per-round sampler outputs (debug/tests)
@@ -395,6 +396,9 @@ class RenderEngine:
         L.call("mli_rgb_bwd", L.RgbBwdArgs(R, N, L.ptr(dz4), L.ptr(self.wbwd), L.ptr(hd["masks"]), L.ptr(dzT),
                                            L.ptr(dz4T)))
         # weight gradients (packed-k space), zeroed then accumulated by split-K atomics
+        if self.gate_wgrad:  # Trainer.prefetch(gate="wgrad"): next geometry may start here
+            self.gate_event = torch.cuda.Event()
+            self.gate_event.record()
         dwbuf = self._buf("dw", (self._dw_total(),))
         dwbuf.zero_()
         jobs, ad = self._wgrad_plan(dzT, dz4T, hd, dwbuf, flat, grad_out, S)

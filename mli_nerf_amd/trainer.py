@@ -159,6 +159,15 @@ class Trainer:
             if model.neural_sdf.c2f is not None:   # neuralangelo/trainer.py:30-32
                 model.neural_sdf.warm_up_end = o.sched.warm_up_end
         self._grad_table = None
+        self._side = None      # prefetch stream (stage-b geometry of the next batch)
+        self._pending = []     # prefetched geometries not yet consumed by train_step
+        self._pf_lane = 0
+        # where the side stream may start the prefetched geometry: "call" (when prefetch is
+        # called: draw, prefetch, then train_step the previous batch), "heads" (after the
+        # heads forward of the last train_step) or "wgrad" (after its heads backward); with
+        # the last two, prefetch is called after train_step
+        self.prefetch_gate = "call"
+        self._gate_ev = None
         self.sched = o.sched
         self.current_iteration = 0
         self.current_epoch = 0
@@ -187,11 +196,70 @@ class Trainer:
         else:
             sdf.set_normal_epsilon()
 
+    def prefetch(self, data, u=None):
+        """Stage-b software pipeline: issue ``data``'s geometry (rays, the hierarchical sampling
+        rounds and the FIELD pass) on a side stream, into a spare engine buffer lane, so that it
+        runs under the heads / backward of the step issued next.  In stage b the geometry reads
+        only the frozen SDF and hash table (NeuralLumen/model.py:422-438 trains neural_rgb
+        alone), so it does not depend on the optimiser step in flight.  ``train_step(data)``
+        with the same dict then runs the heads onward on the prefetched geometry; its results
+        equal the unpipelined step's on the same ``u`` (tests/test_gpu_parity.py).
+
+        Call order: draw the batch, ``prefetch`` it, then ``train_step`` the previous batch.
+        The side stream waits for an event recorded here on the current stream, i.e. after
+        every step issued so far, so lane L is rewritten only once the step that read it two
+        prefetches ago has been issued ahead of it.  A no-op outside the fused stage-b path."""
+        m = self.model
+        if self.stage != "b" or not set(self.weights) <= FUSED_LOSSES:
+            return
+        if len(self._pending) >= 2:
+            raise RuntimeError("prefetch: two batches already prefetched and not yet trained on")
+        m.train()
+        if m.engine is None:
+            m.prepare()
+        eng = m.engine
+        dev = m.flat.device
+        main = torch.cuda.current_stream(dev)
+        if self._side is None or self._side.device != dev:
+            self._side = torch.cuda.Stream(device=dev)
+        ready = self._gate_ev if self.prefetch_gate != "call" else None
+        if ready is None:
+            ready = torch.cuda.Event()
+            ready.record(main)
+        self._gate_ev = None
+        side = self._side
+        side.wait_event(ready)
+        lane = ("pf", self._pf_lane)
+        self._pf_lane ^= 1
+        prev = eng._bufs
+        try:
+            with torch.cuda.stream(side):
+                for k in ("ray_idx", "pose", "intr", "pose_light"):
+                    data[k].record_stream(side)
+                eng.use_lane(lane)
+                rays = eng.rays(data["pose"], data["intr"], data["pose_light"], data["ray_idx"],
+                                m.image_size_train[1])
+                dists = eng.sample(rays, m.stratified_uniforms(data, u))
+                fld = eng.field(rays, dists, True)
+        finally:
+            eng._bufs = prev
+        done = torch.cuda.Event()
+        done.record(side)
+        self._pending.append((data, lane, rays, dists, fld, done))
+
+    def _take_prefetched(self, data):
+        for i, pf in enumerate(self._pending):
+            if pf[0] is data:
+                del self._pending[: i + 1]  # older unconsumed prefetches are dropped
+                return pf[1:]
+        return None
+
     def train_step(self, data, u=None, return_outputs=False):
         """One stage-b iteration.  Hot path: render -> fused losses + output gradients
         (mli_stage_b_loss) -> heads backward -> all-reduce -> fused AdamW, no torch autograd.
         Loss configurations the fused kernel does not cover take the autograd path (the
-        reference's loss code on Model.forward's outputs)."""
+        reference's loss code on Model.forward's outputs).  A batch handed to ``prefetch``
+        earlier reuses its prefetched geometry (``u`` is then the one given to prefetch)."""
         self._start_of_iteration()
         self.model.train()
         if self.stage == "a":
@@ -199,12 +267,34 @@ class Trainer:
         if not set(self.weights) <= FUSED_LOSSES:
             return self.train_step_autograd(data, u)
         m = self.model
+        pf = self._take_prefetched(data)
+        prev = m.engine._bufs if m.engine is not None else None
+        try:
+            return self._train_step_b(data, u, return_outputs, pf)
+        finally:
+            if prev is not None:
+                m.engine._bufs = prev
+
+    def _train_step_b(self, data, u, return_outputs, pf):
+        m = self.model
         m.prepare()
         m.image_width = m.image_size_train[1]
-        st = m.engine.render(data, m.s_var.detach(), m.progress, True, u=m.stratified_uniforms(data, u),
-                             W=m.image_width)
-        m._last_state = st
         eng = m.engine
+        if pf is None:
+            st = eng.render(data, m.s_var.detach(), m.progress, True, u=m.stratified_uniforms(data, u),
+                            W=m.image_width)
+        else:
+            lane, rays, dists, fld, done = pf
+            torch.cuda.current_stream(m.flat.device).wait_event(done)
+            eng.use_lane(lane)
+            hd = eng.heads(rays, dists, fld, True)
+            comp = eng.composite(rays, dists, fld, hd, m.s_var.detach(), m.progress, True)
+            st = (rays, dists, fld, hd, comp)
+        if self.prefetch_gate == "heads":
+            self._gate_ev = torch.cuda.Event()
+            self._gate_ev.record()
+        eng.gate_wgrad = self.prefetch_gate == "wgrad"
+        m._last_state = st
         rays, dists, fld, hd, comp = st
         N, R = dists.shape
         d_rgb, d_o_r = eng._buf("d_rgb", (R, 3)), eng._buf("d_o_r", (R, 3))
@@ -228,6 +318,8 @@ class Trainer:
         if self._grad is None or self._grad.device != m.flat.device:
             self._grad = torch.empty_like(m.flat.detach())  # every element is written by the backward
         grad = eng.backward(st, d_rgb, d_o_r, d_o_s, d_o_re, m.flat, m._sdf_l1(), self._grad)
+        if eng.gate_wgrad:
+            self._gate_ev, eng.gate_event = eng.gate_event, None
         grad = reduce_gradients(grad, self.world_size)
         m.flat.grad = grad
         self.optim.step(grad, self.lr())
