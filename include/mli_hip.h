@@ -35,7 +35,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mli_stream_t; /* == hipStream_t */
 
-#define MLI_ABI_VERSION 6
+#define MLI_ABI_VERSION 7
 #define MLI_HIDDEN 256
 #define MLI_LEVELS 16
 #define MLI_LEVEL_FEAT 8
@@ -478,7 +478,9 @@ int mli_grad_assemble(const mli_assemble_args* a, mli_stream_t s);
 typedef struct {
   float* p; const float* g; float* m; float* v;
   int64_t n;
-  float lr, beta1, beta2, eps, weight_decay;
+  double lr, beta1, beta2, eps, weight_decay; /* double, as torch's Python scalars: the step
+                           coefficients (1 - beta, lr / bias correction ...) are formed in double
+                           and rounded to fp32 once, as torch.optim.AdamW does */
   int step;               /* 1-based step after increment */
   uint16_t* p16;          /* optional fp16 copy of the updated p (hash-table shadow), or NULL */
 } mli_adamw_args;

@@ -11,6 +11,7 @@ P = C.c_void_p
 I32 = C.c_int
 I64 = C.c_int64
 F32 = C.c_float
+F64 = C.c_double
 
 
 class GridLevels(C.Structure):
@@ -114,8 +115,8 @@ class AssembleArgs(C.Structure):
 
 
 class AdamwArgs(C.Structure):
-    _fields_ = [("p", P), ("g", P), ("m", P), ("v", P), ("n", I64), ("lr", F32), ("beta1", F32),
-                ("beta2", F32), ("eps", F32), ("weight_decay", F32), ("step", I32), ("p16", P)]
+    _fields_ = [("p", P), ("g", P), ("m", P), ("v", P), ("n", I64), ("lr", F64), ("beta1", F64),
+                ("beta2", F64), ("eps", F64), ("weight_decay", F64), ("step", I32), ("p16", P)]
 
 
 class CastArgs(C.Structure):
@@ -170,7 +171,7 @@ class FragRowsArgs(C.Structure):
                 ("ld", I64), ("col0", I64), ("row0", I32)]
 
 
-ABI_VERSION = 6  # include/mli_hip.h MLI_ABI_VERSION
+ABI_VERSION = 7  # include/mli_hip.h MLI_ABI_VERSION
 
 ENTRY_POINTS = {
     "mli_rays": RaysArgs, "mli_hashgrid_fwd": HashgridArgs, "mli_sdf": SdfArgs,

@@ -96,3 +96,36 @@ def test_abi_rejects_bad_shapes_and_accepts_empty():
     L.call("mli_sdf", L.SdfArgs(0, 0, 32, None, None, None, None, None, levels, None, 0.0, 1.0, 1.0,
                                 1000.0, 0, None, None, None, None, None, 16))
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("n,offset", [(1 << 20, 0), (1000003, 0), (4099, 1), (3, 0)])
+def test_adamw_matches_torch(n, offset):
+    """mli_adamw (one parameter per lane; sizes cover whole and ragged blocks and an unaligned
+    view) against torch.optim.AdamW (the reference's optimizer,
+    the configs' optim: AdamW lr 1e-3, wd 1e-2) over three steps, with the fp16
+    shadow of the updated parameters.  fp32 elementwise: 3e-8 + 1e-6 |p|; shadow exact."""
+    _need_gpu()
+    from mli_nerf_amd.trainer import FusedAdamW
+    g0 = torch.Generator().manual_seed(n)
+    base = torch.randn(n + offset, generator=g0).to(DEV)
+    p = base[offset:]  # offset 1: a view that is only 4 B aligned
+    ref = p.detach().clone().requires_grad_(True)
+    opt = torch.optim.AdamW([ref], lr=1e-3, weight_decay=1e-2)
+    fused = FusedAdamW(p, lr=1e-3, weight_decay=1e-2)
+    p16 = torch.empty(n + offset, dtype=torch.float16, device=DEV)[offset:]
+    for step in range(3):
+        grad = torch.randn(n, generator=g0).to(DEV)
+        ref.grad = grad.clone()
+        opt.step()
+        fused.step(grad, 1e-3, p16=p16)
+    torch.cuda.synchronize()
+    # the per-step update is lr * m / denom ~ 1e-3: a few fp32 ulps of it (sqrt / divide order
+    # against torch's addcdiv) plus 1e-6 of |p|
+    err = ((p - ref.detach()).abs() - 1e-6 * ref.detach().abs()).max().item()
+    assert err < 3e-8, err
+    assert torch.equal(p16, p.half())
+    # moments: 1-2 fp32 ulps (fused multiply-add against torch's lerp / addcmul rounding)
+    dm = (fused.m - opt.state[ref]["exp_avg"]).abs().max().item()
+    v_ref = opt.state[ref]["exp_avg_sq"]
+    dv = ((fused.v - v_ref).abs() / v_ref.clamp(min=1e-12)).max().item()
+    assert dm < 2e-7 and dv < 2.5e-7, (dm, dv)
