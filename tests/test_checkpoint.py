@@ -71,3 +71,20 @@ def test_stage_a_checkpoint_warm_starts_stage_b(tmp_path):
         else:
             assert torch.equal(sb[k], v), k
     assert not res.unexpected_keys or all(k.startswith("neural_rgb") for k in res.unexpected_keys)
+
+
+def test_prefetch_is_a_no_op_outside_the_fused_stage_b_path():
+    """Trainer.prefetch only pipelines the fused stage-b step: in stage a (the geometry is being
+    trained, so the next batch's sampling depends on this step's update) and for loss configs the
+    fused kernel does not cover it issues nothing, and train_step finds no prefetched geometry."""
+    from mli_nerf_amd.trainer import Trainer
+    cfg_a, ma = _model("a")
+    tra = Trainer(cfg_a, ma)
+    batch = synthetic.make_batch(32, frame=1)
+    tra.prefetch(batch)
+    assert tra._pending == [] and tra._take_prefetched(batch) is None
+    cfg_b, mb = _model("b")
+    trb = Trainer(cfg_b, mb)
+    trb.weights["unfused_term"] = 1.0
+    trb.prefetch(batch)
+    assert trb._pending == []
