@@ -57,11 +57,6 @@ MLI_FI void ring_issue(Ring& r, uint8_t* lds, Bytes&& bytes) {
   const int nb = bytes(real ? r.next : r.n - 1);
   const uint8_t* s = real ? r.src : r.last;
   uint8_t* dst = lds + (r.next % NSLOT) * SLOT + wave * 1024;
-#ifdef MLI_EXP_NODMA  // knockout experiment (tools/kbench_fwd.sh): weights after the prologue stale
-  if (r.next >= DIST)
-    ;
-  else
-#endif
 #pragma unroll
   for (int u = 0; u < GLDS; ++u) glds16(s + min(u * 8192 + wave * 1024 + lane * 16, nb - 16), dst + u * 8192);
   if (real) r.src += nb;
@@ -92,15 +87,11 @@ struct Stager {
 MLI_FI void stage_tile(Stager& sg, uint8_t* lds, const f32x16& v, uint16_t* dst, int lane) {
   const int wave = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
   uint8_t* sb = lds + STAGE_OFF + sg.buf * STAGE + (4 * h) * SROW + (wave * 32 + c) * 2;
-#ifndef MLI_EXP_NOSTAGE
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const f16 x = (f16)v[i];
     *reinterpret_cast<uint16_t*>(sb + ((i & 3) + 8 * (i >> 2)) * SROW) = __builtin_bit_cast(uint16_t, x);
   }
-#else
-  if (v[0] == 1234.5f) *reinterpret_cast<uint16_t*>(sb) = 1;
-#endif
   sg.pend = dst;
   sg.pbuf = sg.buf;
   sg.buf ^= 1;
@@ -140,12 +131,8 @@ MLI_FI f32x16 chunk_mma(const uint8_t* chunk, const half8* X, int lane) {
     acc[4 * u] = b[0]; acc[4 * u + 1] = b[1]; acc[4 * u + 2] = b[2]; acc[4 * u + 3] = b[3];
   }
   const half8* w = reinterpret_cast<const half8*>(chunk) + lane;
-#ifndef MLI_EXP_NOMFMA  // knockout experiment: bias only
 #pragma unroll
   for (int q = 0; q < KS; ++q) acc = mfma32(w[q * 64], X[q], acc);
-#else
-  if (acc[0] == 1234.5f) acc = mfma32(w[0], X[0], acc);
-#endif
   return acc;
 }
 
@@ -182,10 +169,8 @@ MLI_FI void run_layer(Ring& rg, uint8_t* lds, Stager& sg, int S, const half8* X,
       if (t - b < 0) break;
       n += stores(t - b) + (b < DIST - 1 ? pre.count(t - b) : 0);
     }
-#ifndef MLI_EXP_NOSYNC  // knockout experiment: no per-phase wait / barrier (results invalid)
     vm_wait(n);
     block_sync();
-#endif
     rg.cur++;
   }
 }

@@ -664,11 +664,10 @@ __global__ __launch_bounds__(MLP_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_arg
 
 // Hash-grid backward, level-outer like encode5_kernel: lane (c, h) = sample c, level 2qq+h.
 // The center's 8 corners take the weighted d enc of every point in the center's cell (one
-// fp32 atomic per corner feature); a tap in another cell scatters its own 64.
-// lv_only >= 0: one level per launch (level-major over the whole sample set, so the atomic
-// working set is one level's gradient -- <= 2^22 entries x 32 B = 128 MiB, Infinity-Cache
-// sized -- instead of the whole 1.46 GB table); each lane half then takes its own tile.
-__global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a, int lv_only) {
+// fp32 atomic per corner feature); a tap in another cell scatters its own 64.  (A level-major
+// variant, one level per launch so the atomic working set is Infinity-Cache sized, measured
+// slower in round 1: 17.8 vs 15.7 ms before the coalesced scatter.)
+__global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
   // per wave: up to 64 run totals (64 floats) + their 8 corner slots, for the coalesced scatter
   __shared__ __attribute__((aligned(16))) float s_vals[4][64 * 64];
   __shared__ uint32_t s_slot[4][64 * 8];
@@ -677,8 +676,7 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a, int 
   uint32_t* tslot = s_slot[wave];
   const int c = lane & 31, h = lane >> 5;
   const int S = a.R * a.N;
-  const bool single = lv_only >= 0;
-  const int tile = single ? (blockIdx.x * 4 + wave) * 2 + h : blockIdx.x * 4 + wave;
+  const int tile = blockIdx.x * 4 + wave;
   if (tile >= S / 32) return;
   const int m = tile * 32 + c;
   const int r = m / a.N, k = m - r * a.N;
@@ -689,20 +687,14 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a, int 
   for (int p = 0; p < TAPS; ++p)
 #pragma unroll
     for (int d = 0; d < 3; ++d) x[p][d] = (q[p][d] + 2.0f) * 0.25f;
-  const int lane_src = single ? c + 32 * (lv_only & 1) : lane;
-  const float* src = a.d_enc + ((size_t)tile * TAPS * 8) * 512 + lane_src * 8;
-  const int n_it = single ? 1 : 8;
+  const float* src = a.d_enc + ((size_t)tile * TAPS * 8) * 512 + lane * 8;
 #pragma unroll 1
-  for (int it = 0; it < n_it; ++it) {
-    const int qq = single ? lv_only >> 1 : it;
-    if (!single && 2 * qq >= a.active_levels) break;
-    const int lv = single ? lv_only : 2 * qq + h;
+  for (int qq = 0; qq < 8; ++qq) {
+    if (2 * qq >= a.active_levels) break;
+    const int lv = 2 * qq + h;
     // a masked level stays in the loop with zero contributions: the coalesced scatter needs
     // every lane of the wave (lane j adds corner j/8 of a run)
-    bool lv_on = lv < a.active_levels;
-#ifdef MLI_EXP_LEVELS_LO  // experiment builds (tools/kbench_a.py): time a level range only
-    lv_on = lv_on && lv >= MLI_EXP_LEVELS_LO && lv < MLI_EXP_LEVELS_HI;
-#endif
+    const bool lv_on = lv < a.active_levels;
     if (!__any(lv_on)) continue;
     const LevelP P = level_params(a.levels, lv);
     const bool dense = level_dense(a.levels, lv);
@@ -726,19 +718,6 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a, int 
       w *= ((cc >> 1) & 1) ? pos[1] : 1.0f - pos[1];
       w *= ((cc >> 2) & 1) ? pos[2] : 1.0f - pos[2];
       return w;
-    };
-    auto scatter = [&](const uint32_t (&g)[3], const float (&G)[8][8]) MLI_LAMBDA_FI {
-#pragma unroll
-      for (int cc = 0; cc < 8; ++cc) {
-        const uint32_t idx = index_of(g[0] + (cc & 1), g[1] + ((cc >> 1) & 1), g[2] + ((cc >> 2) & 1));
-        float* dstp = a.d_table + (size_t)(P.offset + idx) * 8;
-#ifdef MLI_EXP_NO_ATOMICS
-        if (G[cc][0] == 1234.5f) dstp[0] = G[cc][1];
-#else
-#pragma unroll
-        for (int f = 0; f < 8; ++f) unsafeAtomicAdd(dstp + f, G[cc][f]);
-#endif
-      }
     };
     uint32_t g0[3];
     float pos0[3];
@@ -797,9 +776,6 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a, int 
       }
       const uint32_t nx = __shfl_down(key[0], 1), ny = __shfl_down(key[1], 1), nz = __shfl_down(key[2], 1);
       const bool tail = (c0 == 31 || nx != key[0] || ny != key[1] || nz != key[2]) && any;
-#ifdef MLI_EXP_LANE_ATOMICS
-      if (tail) scatter(cellk, V);
-#else
       // Coalesced scatter: the run totals go through LDS so one atomic instruction adds one
       // run's 8 corners x 8 features with 8 consecutive lanes per corner (one 32 B L2 request
       // per corner instead of 8 -- atomics here are request-rate bound, tools/atomic_bench.hip)
@@ -833,17 +809,12 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a, int 
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           if (i0 + u >= ntail) break;
-#ifdef MLI_EXP_NO_ATOMICS
-          if (v[u] == 1234.5f) a.d_table[(size_t)slot[u] * 8 + (lane & 7)] = v[u];
-#else
           if (v[u] != 0.0f) unsafeAtomicAdd(a.d_table + (size_t)slot[u] * 8 + (lane & 7), v[u]);
-#endif
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#endif
     };
 #pragma unroll 1
     for (int p = 1; p < TAPS; ++p) {
@@ -878,10 +849,8 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a, int 
           }
         }
       }
-#ifndef MLI_EXP_NO_TAP_SCATTER
       // a tap outside the center's cell: reduced over the runs of its own cell
       if (__any(!same && lv_on)) run_scatter(g, T, !same && lv_on);
-#endif
     }
     // Samples of a wave are 32 consecutive depths of one ray: lanes sharing the center cell
     // form contiguous runs (a ray crosses a cell once).  Segmented inclusive scan of the 64
@@ -1062,12 +1031,7 @@ extern "C" int mli_hash_bwd(const mli_hash_bwd_args* a, mli_stream_t s) {
   const int S = a->R * a->N;
   if (S <= 0) return 0;
   if (S % 64 != 0 || !a->d_enc || !a->d_table) return (int)hipErrorInvalidValue;
-#ifdef MLI_EXP_LEVEL_MAJOR  // measured slower (17.8 vs 15.7 ms at 4096 x 128): kept as an experiment
-  for (int lv = 0; lv < a->active_levels && lv < MLI_LEVELS; ++lv)
-    hipLaunchKernelGGL(hash_bwd_kernel, dim3((S / 64 + 3) / 4), dim3(256), 0, (hipStream_t)s, *a, lv);
-#else
-  hipLaunchKernelGGL(hash_bwd_kernel, dim3((S / 32 + 3) / 4), dim3(256), 0, (hipStream_t)s, *a, -1);
-#endif
+  hipLaunchKernelGGL(hash_bwd_kernel, dim3((S / 32 + 3) / 4), dim3(256), 0, (hipStream_t)s, *a);
   MLI_LAUNCH_CHECK();
 }
 
