@@ -48,17 +48,35 @@ struct Ring {
   int next, n, cur;     // next chunk to issue, total chunks, chunk being consumed
 };
 
-// GLDS DMAs for chunk r.next into its slot (past the end: a dummy copy of the last chunk
-// into a free slot, so every phase issues the same count).  bytes(c) = size of chunk c.
-template <class Bytes>
+// Wave roles.  ALL: every wave issues its share of the weight DMAs and of the activation
+// flushes, and waits.  Split queues (DMA + STORE): vmcnt retires vector-memory ops in issue
+// order, so a wave that both streams weights and stores activations waits, for every weight
+// chunk, on the activation stores it issued before that chunk's DMAs.  Waves 0-3 (DMA) issue
+// all the LDS-DMA (weights, ReLU masks) and are the only waves that wait on vmcnt in the
+// phase loop; waves 4-7 (STORE) issue all the activation flushes and never wait on them.
+enum Role { ALL = 0, DMA = 1, STORE = 2 };
+
+// The DMAs for chunk r.next into its slot (past the end: a dummy copy of the last chunk into a
+// free slot, so every phase issues the same count).  bytes(c) = size of chunk c.  ALL: GLDS
+// per wave (8 KiB rounds over 8 waves); DMA: 2 GLDS per wave (4 KiB rounds over 4 waves).
+template <int ROLE>
+constexpr int ring_ops() { return ROLE == ALL ? GLDS : ROLE == DMA ? 2 * GLDS : 0; }
+
+template <int ROLE, class Bytes>
 MLI_FI void ring_issue(Ring& r, uint8_t* lds, Bytes&& bytes) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const bool real = r.next < r.n;
   const int nb = bytes(real ? r.next : r.n - 1);
   const uint8_t* s = real ? r.src : r.last;
   uint8_t* dst = lds + (r.next % NSLOT) * SLOT + wave * 1024;
+  if (ROLE == ALL) {
 #pragma unroll
-  for (int u = 0; u < GLDS; ++u) glds16(s + min(u * 8192 + wave * 1024 + lane * 16, nb - 16), dst + u * 8192);
+    for (int u = 0; u < GLDS; ++u) glds16(s + min(u * 8192 + wave * 1024 + lane * 16, nb - 16), dst + u * 8192);
+  } else if (ROLE == DMA) {
+#pragma unroll
+    for (int u = 0; u < 2 * GLDS; ++u)
+      glds16(s + min(u * 4096 + wave * 1024 + lane * 16, nb - 16), dst + u * 4096);
+  }
   if (real) r.src += nb;
   r.next++;
 }
@@ -97,16 +115,21 @@ MLI_FI void stage_tile(Stager& sg, uint8_t* lds, const f32x16& v, uint16_t* dst,
   sg.buf ^= 1;
 }
 
+template <int ROLE>
 MLI_FI void stage_flush(Stager& sg, const uint8_t* lds, int S) {
-  const int row = threadIdx.x >> 5, col = threadIdx.x & 31;
-  const uint8_t* sb = lds + STAGE_OFF + sg.pbuf * STAGE;
+  // ALL: 512 threads x 2 stores; STORE: waves 4-7, 256 threads x 4 stores; DMA: none
+  constexpr int NS = ROLE == ALL ? 2 : ROLE == STORE ? 4 : 0;
+  const int t = ROLE == STORE ? threadIdx.x - 256 : threadIdx.x;
+  const int row = t >> 5, col = t & 31;
+  const uint8_t* sb = lds + STAGE_OFF + sg.pbuf * STAGE + row * SROW + col * 16;
+  uint16_t* g = sg.pend + (size_t)row * S + col * 8;
+  const size_t step = (size_t)(32 / NS) * S;
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int r = row + 16 * u;
-    const u32x4 x = *reinterpret_cast<const u32x4*>(sb + r * SROW + col * 16);
+  for (int u = 0; u < NS; ++u) {
+    const u32x4 x = *reinterpret_cast<const u32x4*>(sb + (32 / NS) * u * SROW);
     // streaming (non-temporal) store: the activations are re-read only by a later kernel, so
     // they should not evict the weight chunks every phase re-reads from L2
-    __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(sg.pend + (size_t)r * S + col * 8));
+    __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(g + u * step));
   }
   sg.pend = nullptr;
 }
@@ -138,24 +161,28 @@ MLI_FI f32x16 chunk_mma(const uint8_t* chunk, const half8* X, int lane) {
 
 // One layer of NT n-tiles over KS k-steps; epi(t, acc) consumes each finished tile.
 // Static store counts (for the counted vmcnt): STAGED = the layer stages its tiles (the
-// flush of tile t-1 at t >= 1 is 2 stores; the flush at t == 0 is decided at run time and
-// not counted), EPI = unconditional global stores per epilogue, MASKED = one mask store at
-// t == NT-1; pre.issue(t) issues pre.count(t) VMEM ops ahead of the weight DMAs.
-template <int KS, int NT, bool STAGED, int EPI, bool MASKED, class Bytes, class Pre, class Epi>
+// flush of tile t-1 at t >= 1; the flush at t == 0 is decided at run time and not counted),
+// EPI = unconditional global stores per epilogue, MASKED = one mask store at t == NT-1;
+// pre.issue(t) issues pre.count(t) VMEM ops ahead of the weight DMAs.  STORE waves never
+// wait in the loop: nothing they issue lands in LDS.
+template <int ROLE, int KS, int NT, bool STAGED, int EPI, bool MASKED, class Bytes, class Pre, class Epi>
 MLI_FI void run_layer(Ring& rg, uint8_t* lds, Stager& sg, int S, const half8* X, int lane, Bytes&& bytes,
                       Pre&& pre, Epi&& epi) {
+  constexpr int FL = ROLE == ALL ? 2 : 0;  // flush stores in this wave's queue
   // VMEM ops a phase issues after its weight DMAs (flush + epilogue stores), per t in the layer
   auto stores = [](int t) MLI_LAMBDA_FI {
-    return ((t > 0 && STAGED) ? 2 : 0) + EPI + ((MASKED && t == NT - 1) ? 1 : 0);
+    return ((t > 0 && STAGED) ? FL : 0) + EPI + ((MASKED && t == NT - 1) ? 1 : 0);
   };
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     pre.issue(t);
-    ring_issue(rg, lds, bytes);
-    if (t == 0) {
-      if (sg.pend) stage_flush(sg, lds, S);
-    } else if (STAGED) {
-      stage_flush(sg, lds, S);
+    ring_issue<ROLE>(rg, lds, bytes);
+    if (ROLE != DMA) {
+      if (t == 0) {
+        if (sg.pend) stage_flush<ROLE>(sg, lds, S);
+      } else if (STAGED) {
+        stage_flush<ROLE>(sg, lds, S);
+      }
     }
     const f32x16 acc = chunk_mma<KS>(lds + (rg.cur % NSLOT) * SLOT, X, lane);
     epi(t, acc);
@@ -163,13 +190,15 @@ MLI_FI void run_layer(Ring& rg, uint8_t* lds, Stager& sg, int S, const half8* X,
     // them may stay in flight -- the weight DMAs of the DIST-1 later phases, the mask DMAs
     // and stores of this and the previous phases (counted inside this layer, lower bound 0
     // across the layer boundary)
-    int n = (DIST - 1) * GLDS + pre.count(t) + stores(t);
+    if (ROLE != STORE) {
+      int n = (DIST - 1) * ring_ops<ROLE>() + pre.count(t) + stores(t);
 #pragma unroll
-    for (int b = 1; b < DIST; ++b) {
-      if (t - b < 0) break;
-      n += stores(t - b) + (b < DIST - 1 ? pre.count(t - b) : 0);
+      for (int b = 1; b < DIST; ++b) {
+        if (t - b < 0) break;
+        n += stores(t - b) + (b < DIST - 1 ? pre.count(t - b) : 0);
+      }
+      vm_wait(n);
     }
-    vm_wait(n);
     block_sync();
     rg.cur++;
   }
@@ -185,9 +214,8 @@ struct NoPre {
 // L1..L3 (24 x KS 16), L4 (1 x KS 16)
 MLI_FI int fwd_bytes(int c) { return (c >= 8 && (c - 8) % 33 < 8) ? CH(19) : CH(16); }
 
-template <bool TRAIN>
-__global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+template <bool TRAIN, int ROLE>
+MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int S = a.R * a.N;
@@ -244,8 +272,8 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
   }
   // prologue: chunks 0 .. DIST-1 in flight, wait for chunk 0
 #pragma unroll
-  for (int d = 0; d < DIST; ++d) ring_issue(rg, lds, bytes);
-  vm_wait((DIST - 1) * GLDS);
+  for (int d = 0; d < DIST; ++d) ring_issue<ROLE>(rg, lds, bytes);
+  if (ROLE != STORE) vm_wait((DIST - 1) * ring_ops<ROLE>());
   block_sync();
 
   Stager sg{nullptr, 0, 0};
@@ -253,7 +281,7 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
 
   // SDF layer 1: feat = softplus(W1 h0 + b1) -> A; frag image scratch (+ x0T rows 0..255)
   uint16_t* ftile = a.feat_frag + (size_t)tile * FRAG_TILE;
-  run_layer<16, 8, TRAIN, 2, false>(rg, lds, sg, S, B, lane, bytes, NoPre{},
+  run_layer<ROLE, 16, 8, TRAIN, 2, false>(rg, lds, sg, S, B, lane, bytes, NoPre{},
                                     [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
     f32x16 v;
 #pragma unroll
@@ -297,13 +325,13 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
         }
       };
     };
-    run_layer<19, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, B, lane, bytes, NoPre{}, relu_epi(A, 0));
-    run_layer<16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, A, lane, bytes, NoPre{}, relu_epi(B, 1));
-    run_layer<16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, B, lane, bytes, NoPre{}, relu_epi(A, 2));
-    run_layer<16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, A, lane, bytes, NoPre{}, relu_epi(B, 3));
+    run_layer<ROLE, 19, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, B, lane, bytes, NoPre{}, relu_epi(A, 0));
+    run_layer<ROLE, 16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, A, lane, bytes, NoPre{}, relu_epi(B, 1));
+    run_layer<ROLE, 16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, B, lane, bytes, NoPre{}, relu_epi(A, 2));
+    run_layer<ROLE, 16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, A, lane, bytes, NoPre{}, relu_epi(B, 3));
     const int no = hd == 2 ? 1 : 3;
     const int off = hd * 3;
-    run_layer<16, 1, false, 0, false>(rg, lds, sg, S, B, lane, bytes, NoPre{},
+    run_layer<ROLE, 16, 1, false, 0, false>(rg, lds, sg, S, B, lane, bytes, NoPre{},
                                       [&](int, const f32x16& acc) MLI_LAMBDA_FI {
       if (h == 0) {
 #pragma unroll
@@ -315,13 +343,21 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
   vm_wait(0);  // no LDS-DMA may land after the workgroup's LDS is released
 }
 
+// waves 0-3 / 4-7 take the DMA / STORE roles (see Role), compiled as two programs
+template <bool TRAIN>
+__global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 8)) rgb_fwd_body<TRAIN, STORE>(a, lds);
+  else rgb_fwd_body<TRAIN, DMA>(a, lds);
+}
+
 // ---------------------------------------------------------------------- backward dX chain
 // chunk sizes: per head W4^T (8 x KS 1), W3^T, W2^T, W1^T (24 x KS 16)
 MLI_FI int bwd_bytes(int c) { return (c % 32) < 8 ? CH(1) : CH(16); }
 constexpr int BWD_CHUNKS = 3 * 32;
 
-__global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+template <int ROLE>
+MLI_FI void rgb_bwd_body(const mli_rgb_bwd_args& a, uint8_t* lds) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int S = a.R * a.N;
@@ -332,21 +368,25 @@ __global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
   const size_t slot = (size_t)k * a.R + r;
   auto bytes = [](int cc) MLI_LAMBDA_FI { return bwd_bytes(cc); };
   // ReLU-mask block of global layer L (= head*4 + li, li = 0..3 runs masks 3, 2, 1, 0): the
-  // workgroup's 8 tiles are contiguous (8 KiB); one 16 B DMA per thread into mask slot L&1
+  // workgroup's 8 tiles are contiguous (8 KiB), DMA'd by the DMA waves (two 16 B per thread)
+  // into mask slot L&1
+  constexpr int MASK_OPS = ROLE == DMA ? 2 : 0;
   auto mask_dma = [&](int L) MLI_LAMBDA_FI {
     const int Lc = min(L, 11);
     const int hd = Lc >> 2, ml = 3 - (Lc & 3);
     const uint8_t* src = reinterpret_cast<const uint8_t*>(a.masks) +
                          (((size_t)(hd * 4 + ml) * tiles + (size_t)blockIdx.x * WAVES) * 64) * 16;
-    glds16(src + threadIdx.x * 16, lds + MASK_OFF + (L & 1) * 8192 + wave * 1024);
+#pragma unroll
+    for (int u = 0; u < MASK_OPS; ++u)
+      glds16(src + u * 4096 + threadIdx.x * 16, lds + MASK_OFF + (L & 1) * 8192 + u * 4096 + wave * 1024);
   };
 
   Ring rg;
   ring_start(rg, a.wbwd, BWD_CHUNKS, bytes);
   mask_dma(0);
 #pragma unroll
-  for (int d = 0; d < DIST; ++d) ring_issue(rg, lds, bytes);
-  vm_wait((DIST - 1) * GLDS);
+  for (int d = 0; d < DIST; ++d) ring_issue<ROLE>(rg, lds, bytes);
+  if (ROLE != STORE) vm_wait((DIST - 1) * ring_ops<ROLE>());
   block_sync();
 
   half8 A[16], B[16];
@@ -375,7 +415,7 @@ __global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
     struct MaskPre {
       decltype(mask_dma)& dma;
       int next_layer;
-      MLI_FI int count(int t) const { return t == 8 - DIST ? 1 : 0; }
+      MLI_FI int count(int t) const { return t == 8 - DIST ? MASK_OPS : 0; }
       MLI_FI void issue(int t) const {
         if (t == 8 - DIST) dma(next_layer);
       }
@@ -396,13 +436,20 @@ __global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
         stage_tile(sg, lds, v, a.dzT + ((size_t)(hd * 4 + layer) * 256 + 32 * t) * S + col0, lane);
       };
     };
-    run_layer<1, 8, true, 0, false>(rg, lds, sg, S, &z4, lane, bytes, pre(0), mask_epi(A, 3, 0));
-    run_layer<16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, pre(1), mask_epi(B, 2, 1));
-    run_layer<16, 8, true, 0, false>(rg, lds, sg, S, B, lane, bytes, pre(2), mask_epi(A, 1, 2));
-    run_layer<16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, pre(3), mask_epi(B, 0, 3));
+    run_layer<ROLE, 1, 8, true, 0, false>(rg, lds, sg, S, &z4, lane, bytes, pre(0), mask_epi(A, 3, 0));
+    run_layer<ROLE, 16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, pre(1), mask_epi(B, 2, 1));
+    run_layer<ROLE, 16, 8, true, 0, false>(rg, lds, sg, S, B, lane, bytes, pre(2), mask_epi(A, 1, 2));
+    run_layer<ROLE, 16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, pre(3), mask_epi(B, 0, 3));
   }
-  stage_flush(sg, lds, opaque_s(a.R * a.N));  // the last tile, made visible by the last phase's barrier
+  // the last tile, made visible by the last phase's barrier
+  stage_flush<ROLE>(sg, lds, opaque_s(a.R * a.N));
   vm_wait(0);
+}
+
+__global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 8)) rgb_bwd_body<STORE>(a, lds);
+  else rgb_bwd_body<DMA>(a, lds);
 }
 
 
@@ -436,7 +483,7 @@ __global__ __launch_bounds__(THREADS) void geo_bwd_kernel(mli_geo_bwd_args a) {
   ring_start(rg, a.wgeo, GEO_CHUNKS, bytes);
   mask_dma(0);
 #pragma unroll
-  for (int d = 0; d < DIST; ++d) ring_issue(rg, lds, bytes);
+  for (int d = 0; d < DIST; ++d) ring_issue<ALL>(rg, lds, bytes);
   vm_wait((DIST - 1) * GLDS);
   block_sync();
 
@@ -481,10 +528,10 @@ __global__ __launch_bounds__(THREADS) void geo_bwd_kernel(mli_geo_bwd_args a) {
       stage_tile(sg, lds, v, a.dzT + ((size_t)layer * 256 + 32 * t) * S + col0, lane);
     };
   };
-  run_layer<1, 8, true, 0, false>(rg, lds, sg, S, &z4, lane, bytes, pre(0), mask_epi(A, 3, 0));
-  run_layer<16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, pre(1), mask_epi(B, 2, 1));
-  run_layer<16, 8, true, 0, false>(rg, lds, sg, S, B, lane, bytes, pre(2), mask_epi(A, 1, 2));
-  run_layer<16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, NoPre{}, mask_epi(B, 0, 3));
+  run_layer<ALL, 1, 8, true, 0, false>(rg, lds, sg, S, &z4, lane, bytes, pre(0), mask_epi(A, 3, 0));
+  run_layer<ALL, 16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, pre(1), mask_epi(B, 2, 1));
+  run_layer<ALL, 16, 8, true, 0, false>(rg, lds, sg, S, B, lane, bytes, pre(2), mask_epi(A, 1, 2));
+  run_layer<ALL, 16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, NoPre{}, mask_epi(B, 0, 3));
   // feat frags (softplus output of SDF layer 1, forward scratch), one tile ahead of its use:
   // tile 0 now, tile t+1 ahead of phase t's weight DMAs (counted as pre-issued VMEM ops)
   const half8* fsrc = reinterpret_cast<const half8*>(a.feat_frag + (size_t)tile * FRAG_TILE) + lane;
@@ -505,7 +552,7 @@ __global__ __launch_bounds__(THREADS) void geo_bwd_kernel(mli_geo_bwd_args a) {
   // dX0 = W0^T dZ0: tiles 0..7 = d feat -> dZ1sdf = d feat * softplus'(z1), with
   // softplus'(z1) = 1 - exp(-100 feat) (torch: z/(z+1), z = e^{100 z1}; 1 past the threshold);
   // tile 8 = rows 256..287 (p 256..258, normal 259..261: (i=3,h=0), (i=0,h=1), (i=1,h=1))
-  run_layer<16, 9, true, 0, false>(rg, lds, sg, S, B, lane, bytes, FeatPre{fsrc, F},
+  run_layer<ALL, 16, 9, true, 0, false>(rg, lds, sg, S, B, lane, bytes, FeatPre{fsrc, F},
                                    [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
     if (t < 8) {
       f32x16 v;
@@ -531,7 +578,7 @@ __global__ __launch_bounds__(THREADS) void geo_bwd_kernel(mli_geo_bwd_args a) {
   });
   // d h0 (layer-1 path) = W1sdf^T dZ1sdf -> frag image (ACC order, as the h0 image)
   uint16_t* dtile = a.dh0_frag + (size_t)tile * FRAG_TILE;
-  run_layer<16, 8, false, 2, false>(rg, lds, sg, S, A, lane, bytes, NoPre{},
+  run_layer<ALL, 16, 8, false, 2, false>(rg, lds, sg, S, A, lane, bytes, NoPre{},
                                     [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
     half8* dst = reinterpret_cast<half8*>(dtile) + (2 * t) * 64 + lane;
     __builtin_nontemporal_store(acc_to_frag(acc, 0), dst);
