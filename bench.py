@@ -7,8 +7,10 @@ backward through the heads and the fused AdamW update (BASELINE.json configs[1])
 Synthetic seeded inputs / random-init weights of the reference architecture (no dataset
 or checkpoint on the box); full-size hash table (log2 T = 22).
 
-Multi-GPU (torchrun): one process per GPU, each rank renders its own image's rays, one
-RCCL all-reduce of the 3.2 MB flat gradient per step (DDP semantics); weak scaling.
+Multi-GPU: one process per GPU (from torch.distributed.run, or spawned here by ``--gpus N``
+when no launcher set WORLD_SIZE); each rank renders its own image's rays, one RCCL all-reduce
+of the 3.2 MB flat gradient (with the step's loss terms and PSNR in its tail) per step (DDP
+semantics); weak scaling, value = all ranks' rays / the slowest rank's time.
 
 Prints ONE JSON line (rank 0).  Extra fields: per-kernel live timings (HIP events on the
 launch stream), the roofline record of the dominant kernel, the CPU-oracle baseline and
@@ -300,11 +302,58 @@ def cpu_baseline(cfg, R_cpu, steps, threads, stage_a=None):
                 s_per_step=t), data, u, float(psnr)
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_workers(n, argv, script=None, poll_s=0.2):
+    """``--gpus N`` without a launcher: start N processes, one per GPU, with the environment
+    torch.distributed.run gives its workers (RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE,
+    MASTER_ADDR=127.0.0.1, MASTER_PORT), and wait for them.  This process never touches the GPU.
+    The workers inherit stdout / stderr (rank 0 prints the JSON line); if one fails the others
+    are stopped (they would wait in a collective forever).  Returns the first non-zero exit
+    code, else 0."""
+    import subprocess
+    script = script or os.path.abspath(__file__)
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]   # poll every process (no short-circuit)
+            if all(c is not None for c in codes):
+                break
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    return rc or next((p.returncode for p in procs if p.returncode), 0)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of this node; without a launcher's WORLD_SIZE, one process per GPU is spawned")
+    ap.add_argument("--steps", type=int, default=200, help="timed steps (200 x ~5 ms: a >= 1 s timed region)")
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="syn_hotdog_b")
     ap.add_argument("--rays", type=int, default=4096)
     ap.add_argument("--fine", type=int, default=16)
@@ -328,6 +377,11 @@ def main():
                     help="stage a (--config syn_hotdog_a): training iteration (sets the coarse-to-fine "
                          "levels, tap epsilon and curvature weight; >= 80000: all 16 levels active)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        n_dev = torch.cuda.device_count()  # counts without initialising the GPU
+        if n_dev < args.gpus:
+            raise SystemExit("--gpus %d: only %d GPU(s) visible" % (args.gpus, n_dev))
+        sys.exit(launch_workers(args.gpus, sys.argv[1:]))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -351,7 +405,7 @@ def main():
     stage_a = model.stage == "a"
     model.load_state_dict(synthetic.make_state_dict(log2T=22, seed=0, heads="rgb" if stage_a else "rgb_r_s"))
     model = model.to(dev)
-    trainer = Trainer(cfg, model, world_size=world)
+    trainer = Trainer(cfg, is_inference=False, model=model, world_size=world)
     if stage_a:
         # steady state of stage a: past the coarse-to-fine ramp (all 16 levels active)
         trainer.current_iteration = args.iteration

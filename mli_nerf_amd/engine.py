@@ -28,8 +28,9 @@ class PathConfig:
 
     def __init__(self, n_coarse=64, n_fine=16, n_hier=4, white_bg=True, bounding="sphere",
                  aabb=(-1, -1, -1, 1, 1, 1), outside_val=1000.0, anneal_end=0.1, log2T=22,
-                 levels=16, min_logres=5, max_logres=11, light_visibility=None):
+                 levels=16, min_logres=5, max_logres=11, light_visibility=None, scale_rule="fp32"):
         self.n_coarse, self.n_fine, self.n_hier = n_coarse, n_fine, n_hier
+        self.scale_rule = scale_rule  # hash-grid level scale rule (hashgrid.level_table)
         self.white_bg, self.bounding, self.aabb = white_bg, bounding, tuple(float(x) for x in aabb)
         self.outside_val, self.anneal_end = outside_val, anneal_end
         self.log2T, self.levels, self.min_logres, self.max_logres = log2T, levels, min_logres, max_logres
@@ -43,7 +44,7 @@ class PathConfig:
 
 
 def _grid_levels(cfg):
-    table, total = level_table(cfg.levels, cfg.log2T, cfg.min_logres, cfg.max_logres)
+    table, total = level_table(cfg.levels, cfg.log2T, cfg.min_logres, cfg.max_logres, cfg.scale_rule)
     g = L.GridLevels()
     for i, (scale, res, size, off) in enumerate(table):
         g.scale[i], g.res[i], g.size[i], g.offset[i] = scale, res, size, off
@@ -61,6 +62,8 @@ class RenderEngine:
     head) with the geometry trained -- hash table, SDF MLP and s_var (backward_a)."""
 
     def __init__(self, cfg, device, stage="b"):
+        if torch.device(device).type != "cuda":
+            raise RuntimeError("RenderEngine runs on the MI355X (libmli_hip.so); the model is on %s" % device)
         self.cfg = cfg
         self.stage = stage
         self.head_specs = layout.HEADS_A if stage == "a" else layout.HEADS
@@ -320,7 +323,22 @@ class RenderEngine:
         comp.update(o)
         return comp
 
+    def stamp(self):
+        """Identifies the current lane's last render: the render state handed out aliases the
+        lane's scratch buffers, so a later render on the same lane overwrites it."""
+        return (id(self._bufs), self._bufs.get("__gen", 0))
+
+    def check_stamp(self, stamp):
+        for bufs in self._lanes.values():
+            if id(bufs) == stamp[0]:
+                if bufs.get("__gen", 0) != stamp[1]:
+                    raise RuntimeError("render state overwritten: another render ran on the same engine lane "
+                                       "between this forward and its backward")
+                return
+        raise RuntimeError("render state of an unknown engine lane")
+
     def render(self, data, s_var, progress, training, u=None, W=512):
+        self._bufs["__gen"] = self._bufs.get("__gen", 0) + 1
         rays = self.rays(data["pose"], data["intr"], data["pose_light"], data["ray_idx"], W)
         dists = self.sample(rays, u)
         fld = self.field(rays, dists, training)

@@ -13,7 +13,13 @@ imaginaire/trainers/base.py:118-119; NeuralLumen/model.py:17-131):
 * ``inference(data)`` renders the full image in ``rand_rays_val`` chunks (:60-111).
 
 All compute runs in libmli_hip.so; the trainable parameters live in ONE flat fp32 buffer
-(``self.flat``), the named ``nn.Parameter``s are views into it.
+(``self.flat``), the named ``nn.Parameter``s are views into it.  Under autograd the backward
+hands each named Parameter its gradient as a view of one flat gradient buffer, so the
+reference trainer's ``AdamW(model.get_param_groups(cfg.optim))``, DDP's gradient hooks and
+``requires_grad`` flags work as on the reference Model (imaginaire/trainers/base.py:118-119,
+450-457; get_trainer.py:70-118), while the fused Trainer steps the flat buffer in one launch.
+Parameters are registered in the reference's order (tests/golden/param_order.json), so a
+torch optimizer state dict indexes the same tensors in both.
 """
 import math
 
@@ -53,15 +59,19 @@ def path_config_from(cfg_model, cfg_data):
                       outside_val=1000.0 * (-1 if inside_out else 1),
                       anneal_end=float(cfg_model.object.s_var.anneal_end),
                       log2T=int(hg.dict_size), levels=int(cfg_model.object.sdf.encoding.levels),
-                      min_logres=int(hg.min_logres), max_logres=int(hg.max_logres))
+                      min_logres=int(hg.min_logres), max_logres=int(hg.max_logres),
+                      scale_rule=str(_cfg_get(hg, "scale_rule", "fp32")))
 
 
 class WNLinear(torch.nn.Module):
-    """Parameter holder with torch weight_norm names (nerf_util.py:176-178)."""
+    """Parameter holder with torch weight_norm names (nerf_util.py:176-178), registered in the
+    order weight_norm leaves them on an nn.Linear: bias, weight_g, weight_v."""
 
     def __init__(self, v, g, b):
         super().__init__()
-        self.weight_g, self.weight_v, self.bias = v_param(g), v_param(v), v_param(b)
+        self.bias = v_param(b)
+        self.weight_g = v_param(g)
+        self.weight_v = v_param(v)
 
 
 class PlainLinear(torch.nn.Module):
@@ -94,7 +104,7 @@ class NeuralSDF(torch.nn.Module):
 
     def __init__(self, pcfg, c2f=None, view=None):
         super().__init__()
-        _, total = level_table(pcfg.levels, pcfg.log2T, pcfg.min_logres, pcfg.max_logres)
+        _, total = level_table(pcfg.levels, pcfg.log2T, pcfg.min_logres, pcfg.max_logres, pcfg.scale_rule)
         self.tcnn_encoding = _Encoding(total * 8)
         k0 = 3 + pcfg.levels * 8
         if view is None:
@@ -155,15 +165,18 @@ class LumenRGB(torch.nn.Module):
 
 class _RenderHeads(torch.autograd.Function):
     """Forward: the whole render on the GPU.  Backward (stage b): composite -> heads dX chain
-    -> dW GEMMs -> weight-norm backward into the flat trainable buffer.  Stage a: the
-    gradients / hessians are differentiable outputs too and the backward runs the geometry
-    chain (Engine.backward_a) into the flat buffer and the hash table."""
+    -> dW GEMMs -> weight-norm backward into one flat fp32 gradient buffer, handed out as
+    per-Parameter views (``params`` = the model's trainable Parameters in flat-layout order).
+    Stage a: the gradients / hessians are differentiable outputs too and the backward runs the
+    geometry chain (Engine.backward_a) into the flat buffer and the hash table.  Inputs whose
+    ``requires_grad`` is off get no gradient (the reference's partial_grad)."""
 
     @staticmethod
-    def forward(ctx, flat, table, model, data, u, progress, training):
+    def forward(ctx, table, model, data, u, progress, training, *params):
         eng = model.engine
         st = eng.render(data, model.s_var.detach(), progress, training, u=u, W=model.image_width)
         ctx.state = st
+        ctx.stamp = eng.stamp()
         ctx.model = model
         ctx.progress = progress
         model._last_state = st
@@ -176,7 +189,11 @@ class _RenderHeads(torch.autograd.Function):
     @staticmethod
     def backward(ctx, d_rgb, d_o_r, d_o_s, d_o_re, d_grads=None, d_hess=None):
         model = ctx.model
+        if ctx.state is None:
+            raise RuntimeError("_RenderHeads: backward through the same render twice")
+        model.engine.check_stamp(ctx.stamp)
         grad = torch.zeros_like(model.flat)
+        gt = None
         if model.stage == "a":
             st = ctx.state
             N, R = st[1].shape
@@ -185,11 +202,12 @@ class _RenderHeads(torch.autograd.Function):
             c = lambda t: None if t is None else t.contiguous()  # noqa: E731
             model.engine.backward_a(st, d_rgb, model.flat.detach(), grad, gt, 0.0, 0.0, ctx.progress,
                                     d_grad_ext=c(d_grads), d_hess_ext=c(d_hess))
-            ctx.state = None
-            return grad, gt, None, None, None, None, None
-        model.engine.backward(ctx.state, d_rgb, d_o_r, d_o_s, d_o_re, model.flat, model._sdf_l1(), grad)
+        else:
+            model.engine.backward(ctx.state, d_rgb, d_o_r, d_o_s, d_o_re, model.flat, model._sdf_l1(), grad)
         ctx.state = None
-        return grad, None, None, None, None, None, None
+        views = [grad[off:off + n].view(shape) if need else None
+                 for (_, shape, off, n), need in zip(model._trainable_items(), ctx.needs_input_grad[6:])]
+        return (gt if ctx.needs_input_grad[0] else None, None, None, None, None, None, *views)
 
 
 class Model(torch.nn.Module):
@@ -214,7 +232,6 @@ class Model(torch.nn.Module):
         self._layout = {name: (shape, off) for name, shape, off in layout.trainable_layout(self.stage)[0]}
         n_train = layout.trainable_layout(self.stage)[1]
         self.register_buffer("flat", torch.zeros(n_train), persistent=False)
-        self.flat.requires_grad_(True)
         c2f = _cfg_get(cfg_model, "object.sdf.encoding.coarse2fine", None)
         c2f = None if c2f is None else {k: c2f[k] for k in ("enabled", "init_active_level", "step") if k in c2f}
         if self.stage == "a":
@@ -246,13 +263,92 @@ class Model(torch.nn.Module):
         """[(name, shape, offset)] of the flat trainable buffer."""
         return layout.trainable_layout(self.stage)[0]
 
+    def _trainable_items(self):
+        """[(name, shape, offset, numel)] in flat-layout order (the autograd inputs)."""
+        return [(n, shape, off, int(np.prod(shape))) for n, shape, off in layout.trainable_layout(self.stage)[0]]
+
+    def trainable_parameters(self):
+        """The named Parameters that are views of the flat buffer, in flat-layout order."""
+        named = dict(self.named_parameters())
+        return [named[n] for n, _, _, _ in self._trainable_items()]
+
     def device(self):
         return self.flat.device
+
+    def set_flat_grad(self, grad):
+        """Publish a flat gradient (the fused Trainer's) as flat.grad and as per-Parameter views,
+        as the autograd backward does."""
+        self.flat.grad = grad
+        for p, (_, shape, off, n) in zip(self.trainable_parameters(), self._trainable_items()):
+            p.grad = grad[off:off + n].view(shape)
+
+    def flat_grad_from_params(self):
+        """The flat gradient behind the named Parameters' .grad (a view of one buffer after the
+        autograd backward; gathered into one otherwise).  None where no Parameter has a grad."""
+        ps = self.trainable_parameters()
+        if all(p.grad is None for p in ps):
+            return None
+        out = torch.zeros_like(self.flat)
+        for p, (_, _, off, n) in zip(ps, self._trainable_items()):
+            if p.grad is not None:
+                out[off:off + n].copy_(p.grad.reshape(-1))
+        return out
+
+    @torch.no_grad()
+    def init_weights(self, seed=0):
+        """The reference's initial weights (imaginaire trainer.init.type 'none': module inits
+        only): SDF MLP geometric init (neuralangelo/utils/mlp.py:71-84, out_bias from the config),
+        tcnn table U(-1e-4, 1e-4), colour heads nn.Linear default init with zero last bias
+        (nerf_util.py:176-183), s_var = init_val; drawn from seeded CPU generators."""
+        from . import synthetic
+        pc = self.pcfg
+        sd = synthetic.make_state_dict(
+            log2T=pc.log2T, seed=seed, s_var=float(self.cfg_model.object.s_var.init_val), enc_std=0.0,
+            table_amp=1e-4, heads="rgb" if self.stage == "a" else "rgb_r_s",
+            out_bias=float(_cfg_get(self.cfg_model, "object.sdf.mlp.out_bias", 0.5)), scale_rule=pc.scale_rule)
+        self.load_state_dict(sd)
+
+    # -------------------------------------------------------------- checkpoints
+    TABLE_KEY = "neural_sdf.tcnn_encoding.params"
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        """nn.Module.load_state_dict, plus the hash-table size rule: the table size depends on
+        the level-5 resolution tcnn derives from its fp32 scale arithmetic (129 here, 45,724,048
+        entries at the default config) or from exact arithmetic (128, 45,674,504); a checkpoint
+        of the other size switches the level table to that rule instead of failing on shape
+        (neuralangelo/utils/modules.py:42-50; SURVEY.md §8c: the tcnn rule is unpinned)."""
+        src = state_dict.get(self.TABLE_KEY)
+        if src is not None and src.numel() != self.neural_sdf.tcnn_encoding.params.numel():
+            self._adopt_table_size(src.numel())
+        return super().load_state_dict(state_dict, strict=strict, assign=assign)
+
+    def _adopt_table_size(self, numel):
+        from .hashgrid import SCALE_RULES
+        pc = self.pcfg
+        sizes = {}
+        for rule in SCALE_RULES:
+            table, total = level_table(pc.levels, pc.log2T, pc.min_logres, pc.max_logres, rule)
+            sizes[rule] = (total * 8, [r for _, r, _, _ in table])
+        match = [r for r, (n, _) in sizes.items() if n == numel]
+        if not match:
+            raise ValueError(
+                "%s has %d elements; this hash-grid config expects %s" % (
+                    self.TABLE_KEY, numel, ", ".join("%d (%d entries x 8; %s scale rule, level resolutions %s)"
+                                                     % (n, n // 8, r, res[:7]) for r, (n, res) in sizes.items())))
+        rule = match[0]
+        import warnings
+        warnings.warn("checkpoint hash table has %d elements: level-5 resolution %d (%s scale rule); the level "
+                      "table follows it" % (numel, sizes[rule][1][5], rule))
+        pc.scale_rule = rule
+        p = self.neural_sdf.tcnn_encoding.params
+        p.data = torch.zeros(numel, dtype=p.dtype, device=p.device)
+        self.engine = None
+        self._sdf_version = None
 
     def _apply(self, fn, recurse=True):
         super()._apply(fn, recurse)
         # re-point the parameter views at the (possibly moved) flat buffer
-        flat = self.flat.detach().requires_grad_(True)
+        flat = self.flat.detach()
         self._buffers["flat"] = flat
         for name, p in self.named_parameters():
             if name in self._layout:
@@ -310,7 +406,7 @@ class Model(torch.nn.Module):
         u = self.stratified_uniforms(data, u)
         self.image_width = self.image_size_train[1]
         table = self.neural_sdf.tcnn_encoding.params
-        res = _RenderHeads.apply(self.flat, table, self, data, u, self.progress, self.training)
+        res = _RenderHeads.apply(table, self, data, u, self.progress, self.training, *self.trainable_parameters())
         return self.outputs(self._last_state, res)
 
     def stratified_uniforms(self, data, u=None):

@@ -44,12 +44,12 @@ def _weight_norm_pair(w):
 
 
 def make_state_dict(log2T=GRID_DEFAULTS["log2T"], seed=0, s_var=3.0, enc_std=1e-2, table_amp=0.1,
-                    heads="rgb_r_s"):
+                    heads="rgb_r_s", out_bias=0.5, scale_rule="fp32"):
     """Reference state-dict keys (no DDP ``module.`` prefix) -> fp32 CPU tensors.
     ``heads``: LumenRGB network_mode -- 'rgb_r_s' (stage b, three heads) or 'rgb' (stage a,
     the single 294 -> 3 head, drawn first from the same stream, so it equals stage b's mlp)."""
     sd = {}
-    table, total = level_table(log2T=log2T)
+    table, total = level_table(log2T=log2T, scale_rule=scale_rule)
     g = _gen(seed * 100 + 5)
     sd["neural_sdf.tcnn_encoding.params"] = _uniform((total * 8,), -table_amp, table_amp, g)
     g = _gen(seed * 100 + 7)
@@ -64,7 +64,7 @@ def make_state_dict(log2T=GRID_DEFAULTS["log2T"], seed=0, s_var=3.0, enc_std=1e-
         sd["neural_sdf.mlp.linears.%d.bias" % li] = torch.zeros(HIDDEN)
     sd["neural_sdf.mlp.linear_sdf.weight"] = (torch.randn(1, HIDDEN, generator=g) * 1e-4
                                               + math.sqrt(math.pi / HIDDEN))
-    sd["neural_sdf.mlp.linear_sdf.bias"] = torch.full((1,), -0.5)
+    sd["neural_sdf.mlp.linear_sdf.bias"] = torch.full((1,), -float(out_bias))
     g = _gen(seed * 100 + 6)
     for name, k_in, k_out in (HEAD_SPECS[:1] if heads == "rgb" else HEAD_SPECS):
         dims = [k_in] + [HIDDEN] * 4 + [k_out]

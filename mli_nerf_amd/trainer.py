@@ -10,10 +10,20 @@ imaginaire/trainers/base.py (train_step, _get_total_loss, checkpoint layout):
   ONE fused HIP kernel over the flat parameter buffer; LR schedule two_steps_with_warmup
   (neuralangelo/utils/misc.py:28-54);
 * multi-GPU: one process per GPU, gradients averaged with ONE all-reduce of the flat
-  gradient buffer (3.2 MB) over RCCL (DDP semantics, get_trainer.py:80-88);
+  gradient buffer (3.2 MB) over RCCL (DDP semantics, get_trainer.py:80-88), the step's loss
+  terms and PSNR riding in the same collective;
 * checkpoints: {"model", "optim", "sched", "epoch", "iteration"} with ``module.``-prefixed
-  model keys and ``latest_checkpoint.txt`` (imaginaire/trainers/base.py:570-607).
+  model keys and ``latest_checkpoint.txt`` (imaginaire/trainers/base.py:570-607); ``optim`` /
+  ``sched`` are torch ``AdamW`` / ``LambdaLR`` state dicts over the reference's parameter order,
+  so either side resumes the other's checkpoints.
+
+Construction follows the plugin call ``trainer_lib.Trainer(cfg, is_inference=..., seed=...)``
+(imaginaire/trainers/utils/get_trainer.py:31-32): the model is built from ``cfg.model.type``
+(imaginaire/trainers/base.py:103-131), ``cfg.model.use_pre_trained`` is loaded and
+``cfg.trainer.partial_grad`` sets the requires_grad flags (NeuralLumen/trainer.py:22-54).
 """
+import importlib
+import math
 import os
 
 import torch
@@ -53,11 +63,17 @@ def curvature_loss(hessians, outside):
 
 
 FUSED_LOSSES = {"render", "eikonal", "curvature", "intrinsic", "regularize_re"}
+FUSED_LOSSES_A = {"render", "eikonal", "curvature"}
 LOSS_NAMES = ("render", "eikonal", "curvature", "intrinsic", "regularize_re")
 
 
 def _c(t):
     return None if t is None else t.contiguous()
+
+
+def _strip_module(sd):
+    """Model keys of an imaginaire checkpoint (saved from the DDP / WrappedModel wrapper)."""
+    return {k[len("module."):] if k.startswith("module.") else k: v for k, v in sd.items()}
 
 
 def stage_b_losses(out, data, weights, ranges=((0.0, 1.0), (0.0, 1.0)), re_factors=(10.0, 1.0, 1.0),
@@ -109,14 +125,14 @@ class FusedAdamW:
                                         self.flat.numel(), float(lr), self.betas[0], self.betas[1], self.eps,
                                         self.wd, self.step_count, L.ptr(p16)))
 
-    def state_dict(self):
-        return {"step": self.step_count, "exp_avg": self.m, "exp_avg_sq": self.v, "lr": self.lr,
-                "weight_decay": self.wd, "betas": self.betas, "eps": self.eps}
+    def resize(self, numel):
+        """Moments for a parameter whose size changed (a table-size rule switch on load)."""
+        if self.m.numel() != numel:
+            self.m = torch.zeros(numel, device=self.m.device)
+            self.v = torch.zeros(numel, device=self.v.device)
 
-    def load_state_dict(self, sd):
-        self.step_count = sd["step"]
-        self.m.copy_(sd["exp_avg"])
-        self.v.copy_(sd["exp_avg_sq"])
+
+N_METRICS = 8  # loss terms (LOSS_NAMES), total, PSNR, spare -- the tail of the gradient buffer
 
 
 def reduce_gradients(grad, world_size, group=None):
@@ -132,11 +148,23 @@ def reduce_gradients(grad, world_size, group=None):
 
 
 class Trainer:
-    """Minimal stage-b trainer: ``train_step(data)`` = forward + loss + backward + AdamW."""
+    """Stage-b / stage-a trainer: ``train_step(data)`` = forward + loss + backward + AdamW."""
 
-    def __init__(self, cfg, model, world_size=1):
+    def __init__(self, cfg, is_inference=True, seed=0, model=None, world_size=None):
         self.cfg = cfg
-        self.model = model
+        self.is_inference = is_inference
+        built = model is None
+        if built:
+            model = self.setup_model(cfg, seed)
+        self.model = self.model_module = model
+        if world_size is None:
+            import torch.distributed as dist
+            world_size = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        self.world_size = world_size
+        if built:  # an injected model is already set up by its caller
+            self._load_pre_trained(cfg)
+        self.partial_grad_keywords = list(cfg.trainer.get("partial_grad", None) or [])
+        self._set_requires_grad()
         self.weights = {k: v for k, v in cfg.trainer.loss_weight.items() if v}
         # stage-a configs have no intrinsic / residual losses (and no parameters for them)
         p = cfg.trainer.get("para_intrinsic_loss", None) or {}
@@ -149,12 +177,14 @@ class Trainer:
         self._scratch = self._grad = None
         o = cfg.optim
         self.stage = getattr(model, "stage", "b")
-        self.optim = FusedAdamW(model.flat, lr=o.params.lr, weight_decay=o.params.weight_decay)
-        self.optim_table = None
+        self.optim = self.optim_table = None
+        if not is_inference:
+            self.optim = FusedAdamW(model.flat, lr=o.params.lr, weight_decay=o.params.weight_decay)
+            if self.stage == "a":
+                # stage a trains the hash table too (one AdamW group, NeuralLumen/model.py:422-438)
+                self.optim_table = FusedAdamW(model.neural_sdf.tcnn_encoding.params, lr=o.params.lr,
+                                              weight_decay=o.params.weight_decay)
         if self.stage == "a":
-            # stage a trains the hash table too (one AdamW group, NeuralLumen/model.py:422-438)
-            self.optim_table = FusedAdamW(model.neural_sdf.tcnn_encoding.params, lr=o.params.lr,
-                                          weight_decay=o.params.weight_decay)
             self.init_curvature = float(cfg.trainer.loss_weight.get("curvature", 0.0))
             if model.neural_sdf.c2f is not None:   # neuralangelo/trainer.py:30-32
                 model.neural_sdf.warm_up_end = o.sched.warm_up_end
@@ -171,8 +201,52 @@ class Trainer:
         self.sched = o.sched
         self.current_iteration = 0
         self.current_epoch = 0
-        self.world_size = world_size
         self.losses, self.metrics = {}, {}
+
+    # ------------------------------------------------------------ construction (reference)
+    @staticmethod
+    def setup_model(cfg, seed=0):
+        """imaginaire/trainers/base.py:103-131: seeded, built from cfg.model.type, moved to this
+        rank's GPU (LOCAL_RANK / cfg.local_rank) when one is present."""
+        torch.manual_seed(seed)
+        lib = importlib.import_module(cfg.model.type)
+        model = lib.Model(cfg.model, cfg.data)
+        model.init_weights(seed)
+        if torch.cuda.is_available():
+            rank = int(os.environ.get("LOCAL_RANK", cfg.get("local_rank", 0) or 0))
+            model = model.to("cuda:%d" % rank)
+        return model
+
+    def _load_pre_trained(self, cfg):
+        """NeuralLumen/trainer.py:27-42: cfg.model.use_pre_trained.pt_filename (a checkpoint or a
+        latest_checkpoint.txt pointer), model weights only, strict=False."""
+        pre = cfg.model.get("use_pre_trained", None)
+        if not pre:
+            return None
+        path = pre["pt_filename"]
+        if path.endswith(".txt"):
+            with open(path) as f:
+                name = f.readline().strip()
+            if not name:
+                raise FileNotFoundError(path)
+            path = os.path.join(os.path.dirname(path), name)
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        return self.model.load_state_dict(_strip_module(sd["model"]), strict=False)
+
+    def _set_requires_grad(self):
+        """NeuralLumen/trainer.py:44-54 (partial_grad keywords); without keywords every
+        parameter of the stage trains (stage a) / the colour heads do (stage b default)."""
+        kw = self.partial_grad_keywords
+        for name, p in self.model.named_parameters():
+            if kw:
+                p.requires_grad_(any(k in name for k in kw))
+
+    def optimized_parameters(self):
+        """[(name, Parameter)] of the reference optimizer, in its order:
+        model.get_param_groups(cfg.optim) (get_trainer.py:106-118)."""
+        groups = self.model.get_param_groups(self.cfg.optim)
+        ids = {id(p) for p in groups}
+        return [(n, p) for n, p in self.model.named_parameters() if id(p) in ids]
 
     def lr(self):
         s = self.sched
@@ -254,18 +328,31 @@ class Trainer:
                 return pf[1:]
         return None
 
-    def train_step(self, data, u=None, return_outputs=False):
-        """One stage-b iteration.  Hot path: render -> fused losses + output gradients
+    def start_of_iteration(self, data, current_iteration):
+        """imaginaire/trainers/base.py:284-296 for a reference-style outer loop: the iteration
+        number and the per-iteration schedules; the batch moved to the model's device."""
+        self.current_iteration = current_iteration
+        dev = self.model.device()
+        return {k: v.to(dev) if torch.is_tensor(v) else v for k, v in data.items()}
+
+    def train_step(self, data, u=None, return_outputs=False, last_iter_in_epoch=False):
+        """One iteration.  Hot path (stage b): render -> fused losses + output gradients
         (mli_stage_b_loss) -> heads backward -> all-reduce -> fused AdamW, no torch autograd.
         Loss configurations the fused kernel does not cover take the autograd path (the
         reference's loss code on Model.forward's outputs).  A batch handed to ``prefetch``
-        earlier reuses its prefetched geometry (``u`` is then the one given to prefetch)."""
+        earlier reuses its prefetched geometry (``u`` is then the one given to prefetch).
+        ``last_iter_in_epoch`` is accepted for the reference loop (grad_accum_iter is 1)."""
+        if self.is_inference:
+            raise RuntimeError("Trainer(is_inference=True) has no optimizer")
         self._start_of_iteration()
         self.model.train()
         if self.stage == "a":
+            if not set(self.weights) <= FUSED_LOSSES_A:
+                raise NotImplementedError("stage a (LumenRGB mode 'rgb') has no outputs for the loss terms %s"
+                                          % sorted(set(self.weights) - FUSED_LOSSES_A))
             return self.train_step_a(data, u, return_outputs)
         if not set(self.weights) <= FUSED_LOSSES:
-            return self.train_step_autograd(data, u)
+            return self._train_step_autograd(data, u)
         m = self.model
         pf = self._take_prefetched(data)
         prev = m.engine._bufs if m.engine is not None else None
@@ -274,6 +361,20 @@ class Trainer:
         finally:
             if prev is not None:
                 m.engine._bufs = prev
+
+    def _grad_buffer(self):
+        """The flat gradient + N_METRICS metric slots: the loss kernel writes the step's loss
+        terms / PSNR into the tail, so ONE all-reduce averages gradients and metrics."""
+        m = self.model
+        n = m.flat.numel()
+        if self._grad is None or self._grad.device != m.flat.device or self._grad.numel() != n + N_METRICS:
+            self._grad = torch.empty(n + N_METRICS, device=m.flat.device)
+        return self._grad[:n], self._grad[n:]
+
+    def _publish(self, lv):
+        self.losses = {k: lv[i] for i, k in enumerate(LOSS_NAMES) if k in self.weights}
+        self.losses["total"] = lv[5]
+        self.metrics["psnr"] = lv[6]
 
     def _train_step_b(self, data, u, return_outputs, pf):
         m = self.model
@@ -295,38 +396,16 @@ class Trainer:
             self._gate_ev.record()
         eng.gate_wgrad = self.prefetch_gate == "wgrad"
         m._last_state = st
-        rays, dists, fld, hd, comp = st
-        N, R = dists.shape
-        d_rgb, d_o_r = eng._buf("d_rgb", (R, 3)), eng._buf("d_o_r", (R, 3))
-        d_o_s, d_o_re = eng._buf("d_o_s", (R, 1)), eng._buf("d_o_re", (R, 3))
-        if self._scratch is None or self._scratch.device != m.flat.device:
-            self._scratch = torch.zeros(16, device=m.flat.device)
-        lv = torch.empty(8, device=m.flat.device)
-        w = self.weights
-        intr = "intrinsic" in w
-        L.call("mli_stage_b_loss", L.LossArgs(
-            R, N, L.ptr(comp["rgb"]), L.ptr(comp["o_r"]), L.ptr(comp["o_s"]), L.ptr(comp["o_re"]),
-            L.ptr(_c(data["image_sampled"])), L.ptr(_c(data.get("pseudo_ref_sampled")) if intr else None),
-            L.ptr(_c(data.get("pseudo_sha_sampled")) if intr else None),
-            L.ptr(_c(data.get("pseudo_visibility_certainty_sampled")) if intr else None),
-            L.ptr(rays["outside"]), L.ptr(fld["grad"]) if "eikonal" in w else None,
-            L.ptr(fld["hess"]) if "curvature" in w else None,
-            w.get("render", 0.0), w.get("eikonal", 0.0), w.get("curvature", 0.0), w.get("intrinsic", 0.0),
-            w.get("regularize_re", 0.0), self.ranges[0][0], self.ranges[0][1], self.ranges[1][0],
-            self.ranges[1][1], self.intr_factors[0], self.intr_factors[1], *self.re_factors,
-            L.ptr(d_rgb), L.ptr(d_o_r), L.ptr(d_o_s), L.ptr(d_o_re), L.ptr(lv), L.ptr(self._scratch)))
-        if self._grad is None or self._grad.device != m.flat.device:
-            self._grad = torch.empty_like(m.flat.detach())  # every element is written by the backward
-        grad = eng.backward(st, d_rgb, d_o_r, d_o_s, d_o_re, m.flat, m._sdf_l1(), self._grad)
+        grad, lv = self._grad_buffer()  # every element is written by the backward / the loss kernel
+        d_rgb, d_o_r, d_o_s, d_o_re = self._fused_losses(st, data, lv)
+        eng.backward(st, d_rgb, d_o_r, d_o_s, d_o_re, m.flat, m._sdf_l1(), grad)
         if eng.gate_wgrad:
             self._gate_ev, eng.gate_event = eng.gate_event, None
-        grad = reduce_gradients(grad, self.world_size)
-        m.flat.grad = grad
+        reduce_gradients(self._grad, self.world_size)   # gradients + metrics, one collective
+        m.set_flat_grad(grad)
         self.optim.step(grad, self.lr())
         self.current_iteration += 1
-        self.losses = {k: lv[i] for i, k in enumerate(LOSS_NAMES) if k in w}
-        self.losses["total"] = lv[5]
-        self.metrics["psnr"] = lv[6]
+        self._publish(lv)
         return m.outputs(st) if return_outputs else None
 
     def _fused_losses(self, st, data, lv):
@@ -354,22 +433,22 @@ class Trainer:
         return d_rgb, d_o_r, d_o_s, d_o_re
 
     def compute_grads_a(self, data, u=None):
-        """Stage-a forward + fused losses + backward (no optimizer step): fills self._grad (flat
-        MLP buffer incl. s_var) and self._grad_table; returns (render state, loss values)."""
+        """Stage-a forward + fused losses + backward (no optimizer step): fills the flat
+        gradient (MLP buffer incl. s_var, metrics in its tail) and self._grad_table; returns
+        (render state, loss values)."""
         m = self.model
         m.prepare()
         m.image_width = m.image_size_train[1]
         st = m.engine.render(data, m.s_var.detach(), m.progress, True, u=m.stratified_uniforms(data, u),
                              W=m.image_width)
         m._last_state = st
-        lv = torch.empty(8, device=m.flat.device)
+        grad, lv = self._grad_buffer()
         d_rgb = self._fused_losses(st, data, lv)[0]
-        if self._grad is None or self._grad.device != m.flat.device:
-            self._grad = torch.empty_like(m.flat.detach())
         table = m.neural_sdf.tcnn_encoding.params
-        if self._grad_table is None or self._grad_table.device != table.device:
+        if self._grad_table is None or self._grad_table.device != table.device or \
+                self._grad_table.numel() != table.numel():
             self._grad_table = torch.empty_like(table.detach())
-        m.engine.backward_a(st, d_rgb, m.flat.detach(), self._grad, self._grad_table,
+        m.engine.backward_a(st, d_rgb, m.flat.detach(), grad, self._grad_table,
                             self.weights.get("eikonal", 0.0), self.weights.get("curvature", 0.0), m.progress)
         return st, lv
 
@@ -381,69 +460,180 @@ class Trainer:
         m = self.model
         st, lv = self.compute_grads_a(data, u)
         eng = m.engine
-        grad = reduce_gradients(self._grad, self.world_size)
+        grad = self._grad[:m.flat.numel()]
+        reduce_gradients(self._grad, self.world_size)
         gtab = reduce_gradients(self._grad_table, self.world_size)
-        m.flat.grad = grad
+        m.set_flat_grad(grad)
         lr = self.lr()
         self.optim.step(grad, lr)
         self.optim_table.step(gtab, lr, p16=eng.table16)
         self.current_iteration += 1
-        self.losses = {k: lv[i] for i, k in enumerate(LOSS_NAMES) if k in self.weights}
-        self.losses["total"] = lv[5]
-        self.metrics["psnr"] = lv[6]
+        self._publish(lv)
         return m.outputs(st) if return_outputs else None
 
     def train_step_autograd(self, data, u=None):
-        """Reference semantics through torch autograd on Model.forward's outputs."""
+        """Reference semantics through torch autograd on Model.forward's outputs (one iteration,
+        schedules included)."""
         self._start_of_iteration()
-        self.model.train()
-        if self.model.flat.grad is not None:
-            self.model.flat.grad = None
-        out = self.model(data, u=u)
+        return self._train_step_autograd(data, u)
+
+    def _train_step_autograd(self, data, u=None):
+        m = self.model
+        m.train()
+        for p in list(m.trainable_parameters()) + [m.neural_sdf.tcnn_encoding.params]:
+            p.grad = None
+        out = m(data, u=u)
         total, losses, psnr = stage_b_losses(out, data, self.weights, self.ranges, self.re_factors,
                                              self.intr_factors)
         total.backward()
-        grad = reduce_gradients(self.model.flat.grad, self.world_size)
+        grad, lv = self._grad_buffer()
+        g = m.flat_grad_from_params()
+        grad.copy_(g) if g is not None else grad.zero_()
+        lv.zero_()
+        for i, k in enumerate(LOSS_NAMES):
+            if k in losses:
+                lv[i] = losses[k].detach()
+        lv[5], lv[6] = total.detach(), psnr.detach()
+        reduce_gradients(self._grad, self.world_size)
+        m.set_flat_grad(grad)
         self.optim.step(grad, self.lr())
         if self.stage == "a":
-            table = self.model.neural_sdf.tcnn_encoding.params
+            table = m.neural_sdf.tcnn_encoding.params
             gtab = reduce_gradients(table.grad, self.world_size)
-            self.optim_table.step(gtab, self.lr(), p16=self.model.engine.table16)
-            table.grad = None
+            self.optim_table.step(gtab, self.lr(), p16=m.engine.table16)
         self.current_iteration += 1
-        self.losses = {k: v.detach() for k, v in losses.items()}
-        self.losses["total"] = total.detach()
-        self.metrics["psnr"] = psnr
+        self._publish(lv)
         return out
 
     # ------------------------------------------------------------ checkpoint layout
-    def save_checkpoint(self, logdir):
-        """imaginaire/trainers/base.py:570-607 file naming + latest_checkpoint.txt."""
+    def _lr_lambda(self, it):
+        s = self.sched
+        return two_steps_with_warmup(it, s.warm_up_end, tuple(s.two_steps), s.gamma)
+
+    def _moment_views(self):
+        """[(name, Parameter, exp_avg view, exp_avg_sq view)] over the reference optimizer's
+        parameters: flat-buffer Parameters map to slices of the fused AdamW's moments, the hash
+        table (stage a) to the table AdamW's."""
+        offs = {n: (off, shape, k) for n, shape, off, k in self.model._trainable_items()}
+        out = []
+        for name, p in self.optimized_parameters():
+            if name in offs:
+                off, shape, k = offs[name]
+                out.append((name, p, self.optim.m[off:off + k].view(shape), self.optim.v[off:off + k].view(shape)))
+            elif self.optim_table is not None and p is self.model.neural_sdf.tcnn_encoding.params:
+                out.append((name, p, self.optim_table.m, self.optim_table.v))
+            else:
+                raise RuntimeError("optimized parameter %s is not trained by this build's optimizer" % name)
+        return out
+
+    def optim_state_dict(self):
+        """torch.optim.AdamW.state_dict() of the reference optimizer (get_trainer.py:106-150,
+        imaginaire/trainers/base.py:601-607): per-parameter state indexed in
+        model.get_param_groups(cfg.optim) order, one param group with the LambdaLR
+        initial_lr; the group keys come from this torch version's own AdamW."""
+        views = self._moment_views()
+        lr0 = float(self.cfg.optim.params.lr)
+        probe = torch.optim.AdamW([torch.nn.Parameter(torch.zeros(1))], lr=lr0, betas=self.optim.betas,
+                                  eps=self.optim.eps, weight_decay=self.optim.wd)
+        group = dict(probe.state_dict()["param_groups"][0])
+        group.update(lr=lr0 * self._lr_lambda(self.current_iteration), initial_lr=lr0,
+                     params=list(range(len(views))))
+        state = {}
+        if self.optim.step_count > 0:
+            for i, (_, _, m, v) in enumerate(views):
+                state[i] = {"step": torch.tensor(float(self.optim.step_count)),
+                            "exp_avg": m.detach().cpu().clone(), "exp_avg_sq": v.detach().cpu().clone()}
+        return {"state": state, "param_groups": [group]}
+
+    def sched_state_dict(self):
+        """torch.optim.lr_scheduler.LambdaLR.state_dict() in iteration mode
+        (neuralangelo/utils/misc.py:28-54 two_steps_with_warmup; last_epoch = iteration)."""
+        from torch.optim.lr_scheduler import LambdaLR
+        lr0 = float(self.cfg.optim.params.lr)
+        probe = torch.optim.AdamW([torch.nn.Parameter(torch.zeros(1))], lr=lr0)
+        sched = LambdaLR(probe, self._lr_lambda)
+        sched.last_epoch = self.current_iteration
+        sched._step_count = self.current_iteration + 1
+        sched._last_lr = [lr0 * self._lr_lambda(self.current_iteration)]
+        return sched.state_dict()
+
+    def load_optim_state_dict(self, osd):
+        """Accepts torch AdamW state dicts (this build's or the reference's) and the round-1
+        layout {"step", "exp_avg", "exp_avg_sq"} of the flat buffer; anything else raises."""
+        if "state" in osd and "param_groups" in osd:
+            views = self._moment_views()
+            idx = [i for g in osd["param_groups"] for i in g["params"]]
+            if len(idx) != len(views):
+                raise ValueError("optimizer state covers %d parameters, the model trains %d"
+                                 % (len(idx), len(views)))
+            step = 0
+            for i, (name, p, m, v) in zip(idx, views):
+                st = osd["state"].get(i)
+                if not st:
+                    m.zero_()
+                    v.zero_()
+                    continue
+                if tuple(st["exp_avg"].shape) != tuple(m.shape):
+                    raise ValueError("optimizer state of %s has shape %s, expected %s"
+                                     % (name, tuple(st["exp_avg"].shape), tuple(m.shape)))
+                m.copy_(st["exp_avg"])
+                v.copy_(st["exp_avg_sq"])
+                step = int(float(st["step"]))
+            self.optim.step_count = step
+            if self.optim_table is not None:
+                self.optim_table.step_count = step
+        elif "exp_avg" in osd:
+            self.optim.step_count = int(osd["step"])
+            self.optim.m.copy_(osd["exp_avg"])
+            self.optim.v.copy_(osd["exp_avg_sq"])
+        else:
+            raise ValueError("unknown optimizer state layout (keys %s)" % sorted(osd))
+
+    def save_checkpoint(self, logdir, latest=False):
+        """imaginaire/trainers/base.py:570-607: file naming (or latest_checkpoint.pt),
+        latest_checkpoint.txt, {model, optim, sched, epoch, iteration} with ``module.`` keys."""
         os.makedirs(logdir, exist_ok=True)
-        name = "epoch_{:05}_iteration_{:09}_checkpoint.pt".format(self.current_epoch, self.current_iteration)
-        sd = {"module." + k: v for k, v in self.model.state_dict().items()}
-        ck = dict(model=sd, optim=self.optim.state_dict(), sched={"last_epoch": self.current_iteration},
-                  epoch=self.current_epoch, iteration=self.current_iteration)
-        if self.optim_table is not None:  # stage a: the hash table's AdamW moments
-            ck["optim_table"] = self.optim_table.state_dict()
+        name = "latest_checkpoint.pt" if latest else \
+            "epoch_{:05}_iteration_{:09}_checkpoint.pt".format(self.current_epoch, self.current_iteration)
+        sd = {"module." + k: v.detach().cpu() for k, v in self.model.state_dict().items()}
+        ck = dict(model=sd, epoch=self.current_epoch, iteration=self.current_iteration)
+        if self.optim is not None:
+            ck.update(optim=self.optim_state_dict(), sched=self.sched_state_dict())
         torch.save(ck, os.path.join(logdir, name))
         with open(os.path.join(logdir, "latest_checkpoint.txt"), "w") as f:
             f.write(name + "\n")
         return os.path.join(logdir, name)
 
-    def load_checkpoint(self, path, resume=True):
+    def load_checkpoint(self, path, resume=True, strict=None, load_opt=True, load_sch=True):
+        """imaginaire Checkpointer.load (base.py:609-652): the model with
+        cfg.checkpoint.strict_resume; with ``resume`` also epoch / iteration (always, when
+        present), the optimizer and the scheduler.  A hash table of the other size rule
+        re-sizes the table optimizer's moments (Model.load_state_dict)."""
         if path.endswith(".txt"):
             with open(path) as f:
                 path = os.path.join(os.path.dirname(path), f.readline().strip())
+        if strict is None:
+            strict = bool(self.cfg.get("checkpoint", {}).get("strict_resume", True))
         sd = torch.load(path, map_location="cpu", weights_only=True)
-        model_sd = {k[len("module."):] if k.startswith("module.") else k: v for k, v in sd["model"].items()}
-        res = self.model.load_state_dict(model_sd, strict=False)
-        if resume and "optim" in sd and "exp_avg" in sd["optim"]:
-            self.optim.load_state_dict(sd["optim"])
-            if self.optim_table is not None and "optim_table" in sd:
-                self.optim_table.load_state_dict(sd["optim_table"])
-            self.current_iteration = sd.get("iteration", 0)
-            self.current_epoch = sd.get("epoch", 0)
+        res = self.model.load_state_dict(_strip_module(sd["model"]), strict=strict)
+        if self.optim_table is not None:
+            self.optim_table.resize(self.model.neural_sdf.tcnn_encoding.params.numel())
+        if resume:
+            self.current_epoch = int(sd.get("epoch", 0))
+            self.current_iteration = int(sd.get("iteration", 0))
+            if load_opt and self.optim is not None and "optim" in sd:
+                self.load_optim_state_dict(sd["optim"])
+            if load_sch and "sched" in sd and "last_epoch" in sd["sched"]:
+                # iteration mode: the LambdaLR step count is the iteration (base.py:637)
+                self.current_iteration = int(sd["sched"]["last_epoch"])
+        return res
+
+    def load_pre_trained(self, path):
+        """NeuralLumen/trainer.py:27-42 warm start (model weights only, strict=False)."""
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        res = self.model.load_state_dict(_strip_module(sd["model"]), strict=False)
+        if self.optim_table is not None:
+            self.optim_table.resize(self.model.neural_sdf.tcnn_encoding.params.numel())
         return res
 
     def test_video(self, dataset, setting1, setting2, output_dir, mode="test",

@@ -28,15 +28,21 @@ PRIMES = (1, 2654435761, 805459861)
 MASK32 = 0xFFFFFFFF
 
 
-def level_table(n_levels=16, log2T=22, base_res=32, per_level_scale=None):
-    """Return a list of (scale(float32), res, size, offset) per level + total entries."""
+def level_table(n_levels=16, log2T=22, base_res=32, per_level_scale=None, scale_rule="fp32"):
+    """Return a list of (scale(float32), res, size, offset) per level + total entries.
+    ``scale_rule='exact'``: the level scale in float64, rounded to fp32 once (the alternative
+    the build accepts for checkpoints whose table size implies a level-5 resolution of 128)."""
     if per_level_scale is None:
         per_level_scale = np.exp((np.log(2.0 ** 11) - np.log(2.0 ** 5)) / (n_levels - 1))
     log2_pls = np.float32(np.log2(np.float32(per_level_scale)))
     table, offset = [], 0
     for lv in range(n_levels):
-        scale = np.float32(np.exp2(np.float32(lv) * log2_pls)) * np.float32(base_res) - np.float32(1.0)
-        scale = np.float32(scale)
+        if scale_rule == "exact":
+            e = lv * np.log2(float(per_level_scale))
+            scale = np.float32(base_res * 2.0 ** (round(e) if abs(e - round(e)) < 1e-9 else e) - 1.0)
+        else:
+            scale = np.float32(np.exp2(np.float32(lv) * log2_pls)) * np.float32(base_res) - np.float32(1.0)
+            scale = np.float32(scale)
         res = int(np.ceil(scale)) + 1
         dense = res ** 3
         size = min(((dense + 7) // 8) * 8, 1 << log2T)

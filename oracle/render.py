@@ -49,6 +49,7 @@ class PathCfg:
     active_levels: int = None       # coarse-to-fine mask (modules.py:91-113); None = all levels
     anneal_levels: int = None       # tap epsilon level (modules.py:102-107); None = all levels
     light_visibility: dict = None   # model.light_visibility when enabled (NeuralLumen/model.py:25-35)
+    scale_rule: str = "fp32"        # hash-grid level scale rule (oracle/hashgrid.py level_table)
 
     @property
     def n_samples(self):
@@ -67,7 +68,8 @@ class PathCfg:
         return 1.0 / res[lv - 1]
 
     def table(self):
-        return hashgrid.level_table(self.levels, self.log2T, 2 ** self.min_logres, self.growth_rate())
+        return hashgrid.level_table(self.levels, self.log2T, 2 ** self.min_logres, self.growth_rate(),
+                                    scale_rule=self.scale_rule)
 
 
 # --------------------------------------------------------------------------------------

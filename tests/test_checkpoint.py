@@ -25,9 +25,11 @@ def _model(stage, seed=0):
 def test_checkpoint_layout_and_round_trip(tmp_path):
     from mli_nerf_amd.trainer import Trainer
     cfg, m = _model("b")
-    tr = Trainer(cfg, m)
+    tr = Trainer(cfg, is_inference=False, model=m)
     tr.current_iteration, tr.current_epoch = 1234, 5
     tr.optim.m.uniform_()
+    tr.optim.v.uniform_()
+    tr.optim.step_count = 1234
     path = tr.save_checkpoint(str(tmp_path))
     assert os.path.basename(path) == "epoch_00005_iteration_000001234_checkpoint.pt"
     assert (tmp_path / "latest_checkpoint.txt").read_text().strip() == os.path.basename(path)
@@ -35,7 +37,7 @@ def test_checkpoint_layout_and_round_trip(tmp_path):
     assert all(k.startswith("module.") for k in ck["model"])
     assert "module.neural_sdf.tcnn_encoding.params" in ck["model"]
     cfg2, m2 = _model("b", seed=1)
-    tr2 = Trainer(cfg2, m2)
+    tr2 = Trainer(cfg2, is_inference=False, model=m2)
     tr2.load_checkpoint(str(tmp_path / "latest_checkpoint.txt"))
     for k, v in m.state_dict().items():
         assert torch.equal(v, m2.state_dict()[k]), k
@@ -45,20 +47,21 @@ def test_checkpoint_layout_and_round_trip(tmp_path):
 def test_stage_a_checkpoint_warm_starts_stage_b(tmp_path):
     from mli_nerf_amd.trainer import Trainer
     cfg_a, ma = _model("a", seed=2)
-    tra = Trainer(cfg_a, ma)
+    tra = Trainer(cfg_a, is_inference=False, model=ma)
     tra.optim_table.v.uniform_()
+    tra.optim.step_count = tra.optim_table.step_count = 500000
     tra.current_iteration = 500000
     path = tra.save_checkpoint(str(tmp_path / "a"))
     # resume stage a: table moments come back
     cfg_a2, ma2 = _model("a", seed=3)
-    tra2 = Trainer(cfg_a2, ma2)
+    tra2 = Trainer(cfg_a2, is_inference=False, model=ma2)
     tra2.load_checkpoint(path)
     assert torch.equal(tra2.optim_table.v, tra.optim_table.v)
     # warm start stage b (no resume): SDF, table and s_var from stage a; heads stay
     cfg_b, mb = _model("b", seed=4)
     heads_before = {k: v.clone() for k, v in mb.state_dict().items() if k.startswith("neural_rgb")}
-    trb = Trainer(cfg_b, mb)
-    res = trb.load_checkpoint(path, resume=False)
+    trb = Trainer(cfg_b, is_inference=False, model=mb)
+    res = trb.load_pre_trained(path)
     sa, sb = ma.state_dict(), mb.state_dict()
     for k in ("neural_sdf.tcnn_encoding.params", "neural_sdf.mlp.linears.0.weight_v", "neural_sdf.mlp.linear_sdf.bias",
               "s_var"):
@@ -79,12 +82,12 @@ def test_prefetch_is_a_no_op_outside_the_fused_stage_b_path():
     fused kernel does not cover it issues nothing, and train_step finds no prefetched geometry."""
     from mli_nerf_amd.trainer import Trainer
     cfg_a, ma = _model("a")
-    tra = Trainer(cfg_a, ma)
+    tra = Trainer(cfg_a, is_inference=False, model=ma)
     batch = synthetic.make_batch(32, frame=1)
     tra.prefetch(batch)
     assert tra._pending == [] and tra._take_prefetched(batch) is None
     cfg_b, mb = _model("b")
-    trb = Trainer(cfg_b, mb)
+    trb = Trainer(cfg_b, is_inference=False, model=mb)
     trb.weights["unfused_term"] = 1.0
     trb.prefetch(batch)
     assert trb._pending == []

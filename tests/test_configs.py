@@ -29,7 +29,7 @@ EXPECT = {  # stage, bounding, white background, loss terms
 def _check(cfg, name):
     stage, bounding, white, losses = EXPECT[name]
     m = Model(cfg.model, cfg.data)
-    t = Trainer(cfg, m)
+    t = Trainer(cfg, is_inference=False, model=m)
     assert m.stage == stage and m.pcfg.bounding == bounding and m.pcfg.white_bg == white
     assert set(t.weights) == losses
     sd = synthetic.make_state_dict(log2T=12, heads="rgb" if stage == "a" else "rgb_r_s")

@@ -112,3 +112,154 @@ def test_shard_ranges_cover_frame():
         packed = torch.randn(7, shard.N_CHANNELS)
         back = shard.pack(shard.unpack(packed))
         assert torch.equal(back, packed)
+
+
+# ----------------------------------------------------------------------------------------
+# Trainer / Model.inference at world size 2 behind the CPU stub engine (tests/stub_engine.py):
+# the product's step and sharding plumbing, with the render kernels stubbed out
+# ----------------------------------------------------------------------------------------
+def _stub_setup():
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import stub_engine
+    from mli_nerf_amd import synthetic
+    from mli_nerf_amd.configs import preset
+    from mli_nerf_amd.model import Model
+    cfg = preset("syn_hotdog_b", rays=32, n_coarse=16, n_fine=4, log2T=12)
+    m = Model(cfg.model, cfg.data)
+    m.load_state_dict(synthetic.make_state_dict(log2T=12))
+    return stub_engine, cfg, m
+
+
+def _step_result(tr, m):
+    head = m.neural_rgb.mlp.linears[0].bias
+    return dict(flat=m.flat.clone(), grad=m.flat.grad.clone(), head_grad=head.grad.clone(),
+                head_grad_is_view=head.grad.untyped_storage().data_ptr() == m.flat.grad.untyped_storage().data_ptr(),
+                world=tr.world_size,
+                psnr=float(tr.metrics["psnr"]), total=float(tr.losses["total"]), render=float(tr.losses["render"]))
+
+
+def _train_worker(rank, port, results):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        from mli_nerf_amd import synthetic
+        from mli_nerf_amd.trainer import Trainer
+        stub, cfg, m = _stub_setup()
+        stub.install()
+        tr = Trainer(cfg, is_inference=False, model=m)   # world size from the process group
+        tr.current_iteration = 10000
+        tr.train_step(synthetic.make_batch(32, frame=rank))
+        results[rank] = _step_result(tr, m)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_trainer_step_world2_stub_engine(monkeypatch):
+    """One fused stage-b step on 2 ranks with different rays: the flat gradient AND the loss /
+    PSNR metrics are averaged by the one all-reduce, the replicas stay bit-identical, and every
+    named Parameter's .grad is a view of the averaged flat gradient."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    results = ctx.Manager().dict()
+    mp.start_processes(_train_worker, args=(port, results), nprocs=WORLD, join=True, start_method="spawn")
+    from mli_nerf_amd import synthetic
+    from mli_nerf_amd.trainer import Trainer
+    local = []
+    for r in range(WORLD):   # each rank's own step, world size 1, same init
+        stub, cfg, m = _stub_setup()
+        stub.install(monkeypatch)
+        tr = Trainer(cfg, is_inference=False, model=m, world_size=1)
+        tr.current_iteration = 10000
+        tr.train_step(synthetic.make_batch(32, frame=r))
+        local.append(_step_result(tr, m))
+    mean_grad = sum(x["grad"] for x in local) / WORLD
+    for r in range(WORLD):
+        res = results[r]
+        assert res["world"] == WORLD
+        torch.testing.assert_close(res["grad"], mean_grad, rtol=0, atol=1e-7)
+        assert torch.equal(res["flat"], results[0]["flat"])
+        for k in ("psnr", "total", "render"):
+            assert abs(res[k] - sum(x[k] for x in local) / WORLD) < 1e-5, k
+        assert res["head_grad_is_view"]
+    assert not torch.equal(local[0]["grad"], local[1]["grad"])  # the ranks' rays differ
+
+
+def _infer_worker(rank, port, results, size):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        results[rank] = _infer(size, install=True)
+    finally:
+        dist.destroy_process_group()
+
+
+def _infer(size, install=False, monkeypatch=None):
+    from mli_nerf_amd import synthetic
+    stub, cfg, m = _stub_setup()
+    stub.install(monkeypatch)
+    stub.install_cpu_streams()
+    m.image_size_val = list(size)
+    m.rand_rays_val = 8
+    b = synthetic.make_batch(1, frame=2)
+    out = m.inference(dict(pose=b["pose"], intr=b["intr"], pose_light=b["pose_light"]))
+    return {k: out[k].clone() for k in ("rgb_map", "o_r_map", "o_s_map", "depth_map", "normal_map", "opacity_map")}
+
+
+@pytest.mark.timeout(300)
+def test_model_inference_world2_stub_engine(monkeypatch):
+    """Model.inference under a world-2 process group: each rank renders one contiguous tile in
+    padded rand_rays_val chunks and ONE all_gather rebuilds every map on every rank, equal to the
+    single-process render (7 x 9 frame: ragged tiles and chunks)."""
+    size = (7, 9)
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    results = ctx.Manager().dict()
+    mp.start_processes(_infer_worker, args=(port, results, size), nprocs=WORLD, join=True, start_method="spawn")
+    saved = (torch.cuda.current_stream, torch.cuda.Stream, torch.cuda.stream, torch.Tensor.record_stream)
+    try:
+        ref = _infer(size, monkeypatch=monkeypatch)
+    finally:
+        torch.cuda.current_stream, torch.cuda.Stream, torch.cuda.stream, torch.Tensor.record_stream = saved
+    for r in range(WORLD):
+        for k, v in ref.items():
+            assert torch.equal(results[r][k], v), (r, k)
+    assert ref["rgb_map"].shape == (1, 3) + size
+
+
+# ----------------------------------------------------------------------------------------
+# bench.py --gpus N without a launcher: the spawn path
+# ----------------------------------------------------------------------------------------
+_WORKER = r'''
+import json, os, sys
+import torch, torch.distributed as dist
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+assert os.environ["LOCAL_RANK"] == str(rank) and os.environ["MASTER_ADDR"] == "127.0.0.1"
+if sys.argv[1:] == ["--fail"] and rank == 1:
+    sys.exit(3)
+dist.init_process_group("gloo")
+t = torch.tensor([float(rank + 1)])
+dist.all_reduce(t)
+if rank == 0:
+    print(json.dumps({"n_gpus": world, "sum": t.item(), "argv": sys.argv[1:]}))
+dist.destroy_process_group()
+'''
+
+
+@pytest.mark.timeout(300)
+def test_bench_launcher_world2(tmp_path, capfd):
+    """bench.launch_workers: N processes with torchrun's environment, rank 0's line on stdout,
+    exit code 0; a failing rank stops the others (they would block in a collective) and its
+    exit code is returned."""
+    import bench
+    w = tmp_path / "worker.py"
+    w.write_text(_WORKER)
+    assert bench.launch_workers(WORLD, ["--steps", "3"], script=str(w)) == 0
+    out = capfd.readouterr().out.strip().splitlines()
+    import json
+    line = json.loads(out[-1])
+    assert line == {"n_gpus": WORLD, "sum": 3.0, "argv": ["--steps", "3"]}
+    assert bench.launch_workers(WORLD, ["--fail"], script=str(w)) == 3

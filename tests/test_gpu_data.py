@@ -71,7 +71,7 @@ def test_feed_drives_stage_b_training():
     model = Model(cfg.model, cfg.data)
     model.load_state_dict(synthetic.make_state_dict(log2T=14, s_var=3.0))
     model = model.to(DEV)
-    trainer = Trainer(cfg, model)
+    trainer = Trainer(cfg, is_inference=False, model=model)
     H, W = cfg.data.train.image_size
     frames = [synthetic.make_batch(8, frame=f) for f in range(2)]
     g = torch.Generator().manual_seed(0)

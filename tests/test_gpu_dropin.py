@@ -1,0 +1,144 @@
+"""The build as a drop-in under the reference's own training code (GPU).
+
+imaginaire builds ``AdamW(model.get_param_groups(cfg.optim))`` (get_trainer.py:106-150), wraps
+the model in DistributedDataParallel (get_trainer.py:70-91), runs ``loss.backward()`` then
+``optimizer.step()`` (imaginaire/trainers/base.py:450-457), with the partial_grad requires_grad
+flags (NeuralLumen/trainer.py:44-54).  These tests drive the build's Model exactly that way:
+
+* 5 steps with torch.optim.AdamW over get_param_groups + autograd end at the same parameters as
+  5 fused ``Trainer.train_step`` calls (tolerance 1e-6 abs: the two paths share the render and
+  the backward kernels; they differ in the loss derivative code -- torch autograd vs the fused
+  loss kernel -- and in the AdamW implementation, both tested to ~1e-7 relative elsewhere);
+* every named Parameter gets .grad as a view of one flat buffer; requires_grad=False gets None;
+* DDP (RCCL, world 1) fires its hooks: the gradients it leaves equal the plain backward's;
+* a render that another render overwrote before its backward raises instead of producing
+  wrong gradients.
+"""
+import os
+import socket
+
+import pytest
+import torch
+
+from mli_nerf_amd import synthetic
+from mli_nerf_amd.configs import preset
+from mli_nerf_amd.model import Model
+from mli_nerf_amd.trainer import Trainer, stage_b_losses, two_steps_with_warmup
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+R, NC, NF, LOG2T = 256, 16, 4, 14
+
+
+def _model(seed=0):
+    cfg = preset("syn_hotdog_b", rays=R, n_coarse=NC, n_fine=NF, log2T=LOG2T)
+    m = Model(cfg.model, cfg.data)
+    m.load_state_dict(synthetic.make_state_dict(log2T=LOG2T, seed=seed))
+    return cfg, m.to(DEV)
+
+
+def _batch(step):
+    d = synthetic.make_batch(R, frame=step)
+    u = synthetic.stratified_uniforms(R, NC, seed=step)
+    return {k: v.to(DEV) for k, v in d.items()}, u.to(DEV)
+
+
+def _losses(tr, out, data):
+    return stage_b_losses(out, data, tr.weights, tr.ranges, tr.re_factors, tr.intr_factors)
+
+
+def test_reference_adamw_matches_fused_trainer():
+    it0 = 10000   # past the LR warm-up: the step uses lr = 1e-3
+    cfg, ma = _model()
+    tra = Trainer(cfg, is_inference=False, model=ma)
+    tra.current_iteration = it0
+    cfg_b, mb = _model()
+    trb = Trainer(cfg_b, is_inference=False, model=mb)   # flags, loss weights and schedules only
+    o = cfg_b.optim
+    s = o.sched
+    lam = two_steps_with_warmup(it0, s.warm_up_end, tuple(s.two_steps), s.gamma)
+    assert lam == 1.0   # LambdaLR factor stays 1 over the 5 steps (misc.py:43-52)
+    opt = torch.optim.AdamW(mb.get_param_groups(o), lr=o.params.lr * lam, weight_decay=o.params.weight_decay)
+    for step in range(5):
+        data, u = _batch(step)
+        tra.train_step(data, u=u)
+        trb.current_iteration = it0 + step
+        trb._start_of_iteration()          # progress, tap epsilon (neuralangelo/trainer.py:65-76)
+        mb.train()
+        out = mb(data, u=u)
+        total, _, _ = _losses(trb, out, data)
+        total.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+    torch.cuda.synchronize()
+    diff = (ma.flat - mb.flat).abs().max().item()
+    moved = (ma.flat - _model()[1].flat).abs().max().item()
+    assert moved > 1e-3, moved      # the 5 steps did update the heads
+    assert diff <= 1e-6, diff
+
+
+def test_named_parameters_get_gradient_views():
+    cfg, m = _model()
+    tr = Trainer(cfg, is_inference=False, model=m)
+    frozen = m.neural_rgb.mlp_s.linears[2].weight_v
+    frozen.requires_grad_(False)
+    data, u = _batch(0)
+    m.train()
+    out = m(data, u=u)
+    _losses(tr, out, data)[0].backward()
+    grads = {}
+    base = None
+    for n, p in m.named_parameters():
+        if not n.startswith("neural_rgb"):
+            assert p.grad is None, n          # frozen geometry (partial_grad neural_rgb)
+            continue
+        if p is frozen:
+            assert p.grad is None
+            continue
+        assert p.grad is not None and p.grad.shape == p.shape, n
+        st = p.grad.untyped_storage().data_ptr()
+        base = st if base is None else base
+        assert st == base, n                 # all views of ONE flat gradient buffer
+        grads[n] = p.grad
+    assert sum(float(g.abs().sum()) for g in grads.values()) > 0
+
+
+def test_ddp_hooks_fire_on_named_parameters():
+    """DistributedDataParallel over RCCL (world 1, broadcast_buffers=False as get_trainer.py:82-88):
+    its reducer hooks see every trainable Parameter's gradient."""
+    import torch.distributed as dist
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(DEV))
+    try:
+        cfg, m = _model()
+        tr = Trainer(cfg, is_inference=False, model=m)
+        ddp = torch.nn.parallel.DistributedDataParallel(m, device_ids=[0], output_device=0, broadcast_buffers=False)
+        data, u = _batch(1)
+        m.train()
+        _losses(tr, ddp(data, u=u), data)[0].backward()
+        ddp_grads = {n: p.grad.clone() for n, p in m.named_parameters() if p.requires_grad}
+        assert len(ddp_grads) == 45 and all(g.abs().sum() > 0 for g in ddp_grads.values())
+        for p in m.parameters():
+            p.grad = None
+        _losses(tr, m(data, u=u), data)[0].backward()
+        for n, p in m.named_parameters():
+            if p.requires_grad:
+                torch.testing.assert_close(ddp_grads[n], p.grad, rtol=1e-6, atol=1e-9)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_overwritten_render_state_raises():
+    cfg, m = _model()
+    tr = Trainer(cfg, is_inference=False, model=m)
+    m.train()
+    d0, u0 = _batch(0)
+    d1, u1 = _batch(1)
+    out0 = m(d0, u=u0)
+    out1 = m(d1, u=u1)           # same engine lane: out0's render state is gone
+    with pytest.raises(RuntimeError, match="overwritten"):
+        _losses(tr, out0, d0)[0].backward()
+    _losses(tr, out1, d1)[0].backward()   # the latest render still backpropagates

@@ -309,7 +309,7 @@ def test_fused_loss_step_matches_autograd_step(case):
     cfg = _preset(config, rays=64, n_coarse=16, n_fine=4, log2T=14)
     u = torch.rand(1, 64, 16).to(DEV)
     dd = to_dev(data)
-    tr = Trainer(cfg, model)
+    tr = Trainer(cfg, is_inference=False, model=model)
     tr.optim.lr = 0.0  # keep the parameters fixed between the two steps
     tr.optim.wd = 0.0
     tr.train_step(dd, u=u)
@@ -343,7 +343,7 @@ def test_prefetch_pipeline_matches_serial_steps(gate):
     runs = []
     for pipelined in (False, True):
         model, sd, _, _, (Hh, W) = build("syn_hotdog_b", R, Nc, 4, 4, 14, 3.0)
-        tr = Trainer(cfg, model)
+        tr = Trainer(cfg, is_inference=False, model=model)
         tr.prefetch_gate = gate
         g = torch.Generator().manual_seed(7)
         batches = [to_dev(synthetic.make_batch(R, H=Hh, W=W, frame=f)) for f in range(3, 8)]

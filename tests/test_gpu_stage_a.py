@@ -45,7 +45,7 @@ def _setup(R, Nc, Nf, it, log2T=14, s_var=3.0):
     sd = synthetic.make_state_dict(log2T=log2T, s_var=s_var, heads="rgb")
     model.load_state_dict(sd)
     model = model.to(DEV)
-    trainer = Trainer(cfg, model)
+    trainer = Trainer(cfg, is_inference=False, model=model)
     trainer.current_iteration = it
     trainer._start_of_iteration()
     data = synthetic.make_batch(R, frame=3)

@@ -59,7 +59,7 @@ def test_train_psnr_curve_matches_oracle():
     model = Model(cfg.model, cfg.data)
     model.load_state_dict(sd)
     model = model.to(DEV)
-    trainer = Trainer(cfg, model)
+    trainer = Trainer(cfg, is_inference=False, model=model)
     psnr_gpu = []
     for d, u in batches:
         trainer.train_step({k: v.to(DEV) for k, v in d.items()}, u=u.to(DEV))

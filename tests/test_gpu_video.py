@@ -55,7 +55,7 @@ def test_render_video_end_to_end(tmp_path):
     model.load_state_dict(synthetic.make_state_dict(log2T=14, s_var=3.0))
     model = model.to(DEV)
     model.rand_rays_val = 96
-    trainer = Trainer(cfg, model)
+    trainer = Trainer(cfg, is_inference=False, model=model)
     dcfg = to_attr({"data": {"root": str(tmp_path), "type": "projects.NeuralLumen.data_blender",
                              "white_background": True,
                              "train": {"image_size": [H, W]}, "val": {"image_size": [H, W], "subset": None}},
@@ -96,11 +96,11 @@ def test_checkpoint_table_shadow_rebuilt(tmp_path):
     cfg = preset("syn_hotdog_a", rays=64, n_coarse=16, n_fine=4, log2T=14)
     src = Model(cfg.model, cfg.data)
     src.load_state_dict(synthetic.make_state_dict(log2T=14, s_var=3.0, heads="rgb", seed=7))
-    path = Trainer(cfg, src).save_checkpoint(str(tmp_path))
+    path = Trainer(cfg, is_inference=False, model=src).save_checkpoint(str(tmp_path))
     model = Model(cfg.model, cfg.data)
     model.load_state_dict(synthetic.make_state_dict(log2T=14, s_var=3.0, heads="rgb", seed=8))
     model = model.to(DEV)
-    tr = Trainer(cfg, model)
+    tr = Trainer(cfg, is_inference=False, model=model)
     tr.current_iteration = 100000
     batch = {k: v.to(DEV) for k, v in synthetic.make_batch(64, frame=1).items()}
     tr.train_step(batch)                       # shadow built from the seed-8 table

@@ -52,7 +52,7 @@ def main():
     model = Model(cfg.model, cfg.data)
     model.load_state_dict(synthetic.make_state_dict(log2T=22))
     model = model.to(dev)
-    tr = Trainer(cfg, model)
+    tr = Trainer(cfg, is_inference=False, model=model)
     batch = {k: v.to(dev) for k, v in synthetic.make_batch(args.rays, frame=0).items()}
     for _ in range(3):
         tr.train_step(batch)
