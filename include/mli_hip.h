@@ -10,6 +10,15 @@
  * re-entrant (no global mutable state) and enqueue on the given stream only, so they
  * can be captured into a hipGraph.
  *
+ * Scratch sizing: every op whose arguments include caller-provided scratch has a host-only
+ * query   int mli_<op>_workspace(const mli_<op>_args* a, int64_t* bytes)   that reads only the
+ * shape / mode fields of `a` (no pointer is dereferenced, no GPU call is made) and writes the
+ * byte size of each scratch buffer into bytes[], in the order listed with the query.
+ *
+ * Determinism: results are bit-reproducible run to run except where an op documents fp32
+ * atomics; those ops (mli_wgrad, mli_hash_bwd) take a `deterministic` flag that switches to a
+ * fixed-order reduction through their workspace.
+ *
  * Layout conventions (R rays, N samples per ray, S = R*N, B = 1 image per rank as in
  * every reference config, syn_hotdog_b.yaml:38):
  *   [R,3]      ray-major xyz
@@ -35,7 +44,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mli_stream_t; /* == hipStream_t */
 
-#define MLI_ABI_VERSION 7
+#define MLI_ABI_VERSION 8
 #define MLI_HIDDEN 256
 #define MLI_LEVELS 16
 #define MLI_LEVEL_FEAT 8
@@ -123,6 +132,8 @@ typedef struct {
                              encode to 0 (stage b / c2f off: MLI_LEVELS)                     */
 } mli_sdf_args;
 int mli_sdf(const mli_sdf_args* a, mli_stream_t s);
+/* bytes[0]: enc (FIELD mode; 0 in SDF mode). */
+int mli_sdf_workspace(const mli_sdf_args* a, int64_t* bytes);
 
 /* ---------------------------------------------------------------- sampling
  * Replaces nerf_util.sample_dists (nerf_util.py:20-38), sample_dists_hierarchical
@@ -170,6 +181,9 @@ typedef struct {
   int n_heads;            /* 3: LumenRGB 'rgb_r_s' (stage b); 1: mode 'rgb' (stage a, head mlp) */
 } mli_rgb_fwd_args;
 int mli_rgb_fwd(const mli_rgb_fwd_args* a, mli_stream_t s);
+/* bytes[0..4]: y, feat_frag, x0T, xT, masks (the last three 0 unless `train` = xT != NULL is
+ * requested by setting a->xT to any non-NULL value before the query). */
+int mli_rgb_fwd_workspace(const mli_rgb_fwd_args* a, int64_t* bytes);
 
 /* ---------------------------------------------------------------- compositing
  * Replaces compute_neus_alphas/_get_iter_cos (neuralangelo/model.py:492-515),
@@ -213,9 +227,14 @@ typedef struct {
   uint16_t* dz4T;         /* [3 heads][4][S] feature-major dZ4 rows (scaled)                */
 } mli_rgb_bwd_args;
 int mli_rgb_bwd(const mli_rgb_bwd_args* a, mli_stream_t s);
+/* bytes[0..1]: dzT, dz4T. */
+int mli_rgb_bwd_workspace(const mli_rgb_bwd_args* a, int64_t* bytes);
 
-/* Weight/bias gradients dW_l = dZ_l^T X_l, db_l = sum dZ_l (split-K MFMA GEMM, fp32 atomics
- * into dw/db which the caller zeroes).  Jobs are described in mli_nerf_amd/engine.py.
+/* Weight/bias gradients dW_l = dZ_l^T X_l, db_l = sum dZ_l (split-K MFMA GEMM).  Default: the
+ * k-slices add into dw/db (caller-zeroed) by fp32 atomics, in arbitrary order.  deterministic:
+ * every k-slice writes its partial tile into the workspace and a second launch sums the slices
+ * in slice order into dw/db (overwritten; no zeroing needed): bit-reproducible.  Jobs are
+ * described in mli_nerf_amd/engine.py.
  * Jobs fall into three launch classes by shape: BIG (M > 32, K <= 256: 256 x 256 tiles),
  * WIDE (M > 32, K > 256: 256 x 320 tiles, the 304-wide layer-0 input) and THIN (M <= 32:
  * 32 x 256); whole-width tiles stream every dZ row once.  `classes` selects which classes
@@ -237,8 +256,12 @@ typedef struct {
   int n_jobs;
   const mli_wgrad_job* jobs; /* HOST array (copied into the kernel arguments) */
   int classes;            /* MLI_WGRAD_* mask */
+  int deterministic;      /* 0: fp32 atomics; 1: slice partials + ordered reduction */
+  float* workspace;       /* deterministic: mli_wgrad_workspace bytes (reused across classes) */
 } mli_wgrad_args;
 int mli_wgrad(const mli_wgrad_args* a, mli_stream_t s);
+/* bytes[0]: workspace (0 unless deterministic): the largest class in `classes`. */
+int mli_wgrad_workspace(const mli_wgrad_args* a, int64_t* bytes);
 
 /* ---------------------------------------------------------------- stage a (geometry training)
  * Backward of the whole render w.r.t. the geometry: replaces autograd through
@@ -264,10 +287,12 @@ typedef struct {
   float* dz4;             /* [N][R][8] scaled */
   float* d_sdf;           /* [N][R] */
   float* d_grad;          /* [N][R][3] */
-  float* d_inv_s_acc;     /* device scalar, zeroed by the caller */
+  float* d_inv_s_part;    /* scratch [R] per-ray d inv_s partials, summed in ray order */
   float* d_s_var;         /* device scalar out: exp(s_var) * d_inv_s */
 } mli_composite_bwd_geo_args;
 int mli_composite_bwd_geo(const mli_composite_bwd_geo_args* a, mli_stream_t s);
+/* bytes[0..3]: dz4, d_sdf, d_grad, d_inv_s_part. */
+int mli_composite_bwd_geo_workspace(const mli_composite_bwd_geo_args* a, int64_t* bytes);
 
 /* dX chain of the single head down to its inputs, then through SDF layer 1:
  * dZ3..dZ0 (feature-major, for the head dW), dX0 -> d feat (frag order) and d normal,
@@ -287,12 +312,15 @@ typedef struct {
   uint16_t* dh0_frag;     /* [S/32][16][64][8] d h0 (scaled, layer-1 path only) */
 } mli_geo_bwd_args;
 int mli_geo_bwd(const mli_geo_bwd_args* a, mli_stream_t s);
+/* bytes[0..5]: dzT, dz4T, d_nrm, dz1T, dh0_frag (and 0). */
+int mli_geo_bwd_workspace(const mli_geo_bwd_args* a, int64_t* bytes);
 
 /* SDF layer 0 + sdf head backward for the 5 points of every sample (center + 4 taps):
  * combines d sdf / d grad (composite), eikonal / curvature gradients, the normalize
  * backward of d normal and the tap stencils into d sdf_i; recomputes layer 0 of every point
  * from the FIELD encodings; writes d enc (fp32, for mli_hash_bwd), dZ0 frag images and the
- * p rows of the layer-0 input (for the dW GEMM) and accumulates dW/db of linear_sdf. */
+ * p rows of the layer-0 input (for the dW GEMM) and dW/db of linear_sdf (per-wave sums in
+ * LDS, per-workgroup partials in `partials`, summed in workgroup order by a second launch). */
 typedef struct {
   int R, N;
   const float* center; const float* ray_unit; const float* dists;
@@ -310,12 +338,15 @@ typedef struct {
   float* d_enc;           /* [S/32][5][8][64][8] fp32 (unscaled) */
   uint16_t* dz0_frag;     /* [5][S/32][16][64][8] scaled dZ0 of the 5 points (ACC order) */
   uint16_t* x0_rows;      /* [131][5S] fp16 layer-0 input rows (p 0..2, enc 3..130); this writes rows 0..2 */
-  float* dw_sdf;          /* [256] scaled, atomics (caller zeroes) */
-  float* db_sdf;          /* [1] scaled, atomics (caller zeroes) */
+  float* dw_sdf;          /* [256] scaled (written) */
+  float* db_sdf;          /* [1] scaled (written) */
   const float* d_grad_ext; /* optional [N][R][3] d loss / d gradients from outside (autograd) */
   const float* d_hess_ext; /* optional [N][R][3] d loss / d hessians from outside (autograd) */
+  float* partials;        /* scratch [workgroups][257] */
 } mli_sdf_bwd_args;
 int mli_sdf_bwd(const mli_sdf_bwd_args* a, mli_stream_t s);
+/* bytes[0..3]: d_enc, dz0_frag, x0_rows, partials. */
+int mli_sdf_bwd_workspace(const mli_sdf_bwd_args* a, int64_t* bytes);
 
 /* W0_enc^T fragments (A operand of d enc = W0_enc^T dZ0; rows ordered so each lane half
  * holds 8 features of one level) -- MLI_SDF_T_PACK_BYTES. */
@@ -328,7 +359,10 @@ int mli_pack_sdf_t(const mli_pack_sdf_t_args* a, mli_stream_t s);
 
 /* Hash-grid backward: d table[(offset_l + idx) * 8 + f] += w_corner * d enc, for the 5
  * points of every sample (taps in the center's cell share its corners: one atomic per
- * corner feature), levels < active_levels.  fp32 atomics into the caller-zeroed grad. */
+ * corner feature), levels < active_levels.  Default: fp32 atomics into the caller-zeroed
+ * d_table.  deterministic: the run totals are added as fixed-point int64 (2^-40 units) into
+ * the caller-zeroed workspace -- integer sums do not depend on their order -- and a second
+ * launch writes d_table = float(sum * 2^-40) (overwritten): bit-reproducible. */
 typedef struct {
   int R, N;
   const float* center; const float* ray_unit; const float* dists;
@@ -337,8 +371,13 @@ typedef struct {
   float eps;
   int active_levels;
   float* d_table;         /* [entries*8] fp32 */
+  int deterministic;
+  int64_t* workspace;     /* deterministic: [entries*8] int64, zeroed by the caller */
+  int64_t n_params;       /* entries*8 (deterministic: the workspace / d_table length) */
 } mli_hash_bwd_args;
 int mli_hash_bwd(const mli_hash_bwd_args* a, mli_stream_t s);
+/* bytes[0]: workspace (0 unless deterministic). */
+int mli_hash_bwd_workspace(const mli_hash_bwd_args* a, int64_t* bytes);
 
 /* Frag image -> feature-major rows: src [tiles][tile_stride halves], k-step q of tile t at
  * src + t*tile_stride + q*512; element (q, lane half h, j) of sample t*32 + (lane & 31) goes
@@ -377,6 +416,8 @@ typedef struct {
   uint8_t* visibility; float* normal_x_light; float* pseudo_shading; /* [R] */
 } mli_light_visibility_args;
 int mli_light_visibility(const mli_light_visibility_args* a, mli_stream_t s);
+/* bytes[0..4]: light_unit, near_l, far_t, inside, inter_pts. */
+int mli_light_visibility_workspace(const mli_light_visibility_args* a, int64_t* bytes);
 
 /* ---------------------------------------------------------------- on-device ray batch
  * Replaces the per-sample CPU draw of NeuralLumen/data.py:120-132 / data_blender.py:179-195
@@ -405,7 +446,7 @@ int mli_ray_batch(const mli_ray_batch_args* a, mli_stream_t s);
  * replaces NeuralLumen/trainer.py:133-149 (_compute_loss) with eikonal/curvature
  * (neuralangelo/utils/misc.py:74-90), intrinsic_loss / regularize_re_loss
  * (NeuralLumen/utils/utils.py:142-174) and _get_total_loss (imaginaire/trainers/base.py:534-544).
- * Gradients are deterministic; loss values are fp32 atomic sums (logging). */
+ * Deterministic: workgroup partial sums go to `scratch` and one launch sums them in order. */
 typedef struct {
   int R, N;
   const float* rgb; const float* o_r; const float* o_s; const float* o_re; /* [R,3],[R,3],[R],[R,3] */
@@ -418,9 +459,12 @@ typedef struct {
   float f_neg, f_pos, e_pos;
   float* d_rgb; float* d_o_r; float* d_o_s; float* d_o_re; /* d total / d output */
   float* losses;          /* [8]: render, eikonal, curvature, intrinsic, regularize_re, total, psnr, mse */
-  float* scratch;         /* [12] device, zeroed once by the caller (left zeroed by every call) */
+  float* scratch;         /* mli_stage_b_loss_workspace bytes: min/max of the pseudo maps + the
+                             workgroup partial sums (no zeroing needed) */
 } mli_loss_args;
 int mli_stage_b_loss(const mli_loss_args* a, mli_stream_t s);
+/* bytes[0]: scratch; bytes[1..4]: d_rgb, d_o_r, d_o_s, d_o_re. */
+int mli_stage_b_loss_workspace(const mli_loss_args* a, int64_t* bytes);
 
 /* ---------------------------------------------------------------- parameters
  * Weight-norm W = g * v / ||v||_row (torch.nn.utils.weight_norm dim=0) folded once per
@@ -445,6 +489,8 @@ typedef struct {
   float* row_scale;       /* scratch [n_layers][256]: g / ||v_row|| (n_out <= 256)           */
 } mli_pack_args;
 int mli_pack(const mli_pack_args* a, mli_stream_t s);
+/* bytes[0]: row_scale. */
+int mli_pack_workspace(const mli_pack_args* a, int64_t* bytes);
 
 /* SDF layer-0 block: fp16 fragments of W0[:, 3:] + fp32 row constants (see layout.py). */
 typedef struct {

@@ -77,7 +77,8 @@ class WgradJob(C.Structure):
 
 
 class WgradArgs(C.Structure):
-    _fields_ = [("S", I32), ("n_jobs", I32), ("jobs", P), ("classes", I32)]
+    _fields_ = [("S", I32), ("n_jobs", I32), ("jobs", P), ("classes", I32), ("deterministic", I32),
+                ("workspace", P)]
 
 
 class LossArgs(C.Structure):
@@ -126,7 +127,7 @@ class CastArgs(C.Structure):
 class CompositeBwdGeoArgs(C.Structure):
     _fields_ = [("R", I32), ("N", I32), ("dists", P), ("far_", P), ("ray_unit", P), ("sdf", P), ("grad", P),
                 ("y", P), ("s_var", P), ("anneal", F32), ("white_bg", I32), ("d_rgb", P), ("grad_scale", F32),
-                ("dz4", P), ("d_sdf", P), ("d_grad", P), ("d_inv_s_acc", P), ("d_s_var", P)]
+                ("dz4", P), ("d_sdf", P), ("d_grad", P), ("d_inv_s_part", P), ("d_s_var", P)]
 
 
 class GeoBwdArgs(C.Structure):
@@ -139,7 +140,8 @@ class SdfBwdArgs(C.Structure):
                 ("grad", P), ("hess", P), ("d_sdf", P), ("d_grad", P), ("d_nrm", P), ("dh0_frag", P), ("enc", P),
                 ("wsdf", P), ("wsdf_t", P), ("eps", F32), ("grad_den", F32), ("hess_den", F32),
                 ("w_eikonal", F32), ("w_curvature", F32), ("grad_scale", F32), ("d_enc", P), ("dz0_frag", P),
-                ("x0_rows", P), ("dw_sdf", P), ("db_sdf", P), ("d_grad_ext", P), ("d_hess_ext", P)]
+                ("x0_rows", P), ("dw_sdf", P), ("db_sdf", P), ("d_grad_ext", P), ("d_hess_ext", P),
+                ("partials", P)]
 
 
 class PackSdfTArgs(C.Structure):
@@ -148,7 +150,8 @@ class PackSdfTArgs(C.Structure):
 
 class HashBwdArgs(C.Structure):
     _fields_ = [("R", I32), ("N", I32), ("center", P), ("ray_unit", P), ("dists", P), ("d_enc", P),
-                ("levels", GridLevels), ("eps", F32), ("active_levels", I32), ("d_table", P)]
+                ("levels", GridLevels), ("eps", F32), ("active_levels", I32), ("d_table", P),
+                ("deterministic", I32), ("workspace", P), ("n_params", I64)]
 
 
 class LightVisibilityArgs(C.Structure):
@@ -171,7 +174,7 @@ class FragRowsArgs(C.Structure):
                 ("ld", I64), ("col0", I64), ("row0", I32)]
 
 
-ABI_VERSION = 7  # include/mli_hip.h MLI_ABI_VERSION
+ABI_VERSION = 8  # include/mli_hip.h MLI_ABI_VERSION
 
 ENTRY_POINTS = {
     "mli_rays": RaysArgs, "mli_hashgrid_fwd": HashgridArgs, "mli_sdf": SdfArgs,
@@ -183,6 +186,14 @@ ENTRY_POINTS = {
     "mli_composite_bwd_geo": CompositeBwdGeoArgs, "mli_geo_bwd": GeoBwdArgs, "mli_sdf_bwd": SdfBwdArgs,
     "mli_pack_sdf_t": PackSdfTArgs, "mli_hash_bwd": HashBwdArgs, "mli_frag_rows": FragRowsArgs,
     "mli_light_visibility": LightVisibilityArgs, "mli_ray_batch": RayBatchArgs,
+}
+
+# host-only scratch-size queries: int mli_<op>_workspace(const args*, int64_t* bytes) -> how many
+# sizes each writes (include/mli_hip.h lists their order)
+WORKSPACE = {
+    "mli_sdf": 1, "mli_rgb_fwd": 5, "mli_rgb_bwd": 2, "mli_wgrad": 1, "mli_composite_bwd_geo": 4,
+    "mli_geo_bwd": 6, "mli_sdf_bwd": 4, "mli_hash_bwd": 1, "mli_light_visibility": 5, "mli_stage_b_loss": 5,
+    "mli_pack": 1,
 }
 
 _lib = None
@@ -199,6 +210,10 @@ def lib():
             fn = getattr(_lib, name)
             fn.argtypes = [C.POINTER(st), P]
             fn.restype = I32
+        for name in WORKSPACE:
+            fn = getattr(_lib, name + "_workspace")
+            fn.argtypes = [C.POINTER(ENTRY_POINTS[name]), C.POINTER(I64)]
+            fn.restype = I32
         _lib.mli_abi_version.restype = I32
         _lib.mli_error_string.restype = C.c_char_p
         _lib.mli_error_string.argtypes = [I32]
@@ -213,6 +228,15 @@ def _variant(name, args):
     if name == "mli_wgrad":
         return {1: ":big", 2: ":wide", 4: ":thin"}.get(args.classes, "")
     return ""
+
+
+def workspace(name, args):
+    """Byte sizes of op ``name``'s scratch buffers for ``args`` (host-only, no GPU call)."""
+    out = (I64 * 8)()
+    rc = getattr(lib(), name + "_workspace")(C.byref(args), out)
+    if rc != 0:
+        raise RuntimeError("%s_workspace failed: %s (%d)" % (name, lib().mli_error_string(rc).decode(), rc))
+    return [int(out[i]) for i in range(WORKSPACE[name])]
 
 
 def ptr(t):

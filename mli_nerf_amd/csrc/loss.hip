@@ -12,9 +12,10 @@
 // which feed mli_composite_bwd.  In stage b eikonal/curvature carry no gradient (frozen SDF).
 //
 // Three launches: min/max of the pseudo maps (one block), per-element terms + gradients with
-// block partial sums folded by fp32 atomics, and a one-thread finalize that also re-zeroes
-// the accumulators for the next call.  The gradients are deterministic; the loss VALUES are
-// sums in atomic order (logging only).
+// one partial sum per workgroup and accumulator, and a finalize that sums the partials in
+// workgroup order (no atomics: values and gradients are bit-reproducible).
+//
+// scratch layout (floats): [0, 4) min/max of sha and cert, [4, 4 + ACC_N * workgroups) partials.
 #include "common.h"
 
 namespace {
@@ -56,8 +57,8 @@ __global__ __launch_bounds__(1024) void minmax_kernel(mli_loss_args a) {
       mn_s = fminf(mn_s, red[0][w]); mx_s = fmaxf(mx_s, red[1][w]);
       mn_c = fminf(mn_c, red[2][w]); mx_c = fmaxf(mx_c, red[3][w]);
     }
-    a.scratch[ACC_N + 0] = mn_s; a.scratch[ACC_N + 1] = mx_s;
-    a.scratch[ACC_N + 2] = mn_c; a.scratch[ACC_N + 3] = mx_c;
+    a.scratch[0] = mn_s; a.scratch[1] = mx_s;
+    a.scratch[2] = mn_c; a.scratch[3] = mx_c;
   }
 }
 
@@ -88,7 +89,7 @@ __global__ __launch_bounds__(256) void terms_kernel(mli_loss_args a, int nb_ray)
       // intrinsic
       float w_sha = 0.f, w_ref = 0.f;
       if (a.w_intrinsic != 0.f) {
-        const float* st = a.scratch + ACC_N;
+        const float* st = a.scratch;
         w_sha = rescale(a.sha[r], st[0], st[1], a.range_sha_lo, a.range_sha_hi);
         const float w_vis = rescale(a.cert[r], st[2], st[3], a.range_vis_lo, a.range_vis_hi);
         w_ref = fminf(w_vis, w_sha);
@@ -138,12 +139,20 @@ __global__ __launch_bounds__(256) void terms_kernel(mli_loss_args a, int nb_ray)
 #pragma unroll
   for (int i = 0; i < ACC_N; ++i) {
     const float v = block_sum(acc[i], redw);
-    if (threadIdx.x == 0 && v != 0.f) atomicAdd(a.scratch + i, v);
+    if (threadIdx.x == 0) a.scratch[4 + (size_t)blockIdx.x * ACC_N + i] = v;
   }
 }
 
-__global__ void finalize_kernel(mli_loss_args a) {
-  float* acc = a.scratch;
+// thread i sums accumulator i over the workgroups, in workgroup order
+__global__ void finalize_kernel(mli_loss_args a, int n_blocks) {
+  __shared__ float acc[ACC_N];
+  if (threadIdx.x < ACC_N) {
+    float t = 0.f;
+    for (int b = 0; b < n_blocks; ++b) t += a.scratch[4 + (size_t)b * ACC_N + threadIdx.x];
+    acc[threadIdx.x] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
   const float R3 = 3.0f * a.R, SN = (float)a.R * a.N;
   const float render = acc[0] / R3 * 3.0f;
   const float mse = acc[1] / R3;
@@ -155,9 +164,10 @@ __global__ void finalize_kernel(mli_loss_args a) {
   o[5] = a.w_render * render + a.w_eikonal * eik + a.w_curvature * curv + a.w_intrinsic * intr + a.w_re * re;
   o[6] = -10.0f * log10f(mse);
   o[7] = mse;
-#pragma unroll
-  for (int i = 0; i < ACC_N; ++i) acc[i] = 0.f;  // ready for the next call
 }
+
+constexpr int NB_SMP = 256;  // workgroups over the R*N samples (eikonal / curvature)
+inline int n_blocks(int R) { return (R + 255) / 256 + NB_SMP; }
 
 }  // namespace
 
@@ -165,10 +175,20 @@ extern "C" int mli_stage_b_loss(const mli_loss_args* a, mli_stream_t s) {
   if (a->R <= 0 || a->N <= 0) return (int)hipErrorInvalidValue;
   if (a->w_intrinsic != 0.f && (a->sha == nullptr || a->cert == nullptr || a->ref == nullptr))
     return (int)hipErrorInvalidValue;
+  if (a->scratch == nullptr) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(minmax_kernel, dim3(1), dim3(1024), 0, (hipStream_t)s, *a);
   const int nb_ray = (a->R + 255) / 256;
-  const int nb_smp = 256;
-  hipLaunchKernelGGL(terms_kernel, dim3(nb_ray + nb_smp), dim3(256), 0, (hipStream_t)s, *a, nb_ray);
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1), 0, (hipStream_t)s, *a);
+  hipLaunchKernelGGL(terms_kernel, dim3(nb_ray + NB_SMP), dim3(256), 0, (hipStream_t)s, *a, nb_ray);
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)s, *a, n_blocks(a->R));
   MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_stage_b_loss_workspace(const mli_loss_args* a, int64_t* bytes) {
+  if (a->R <= 0 || a->N <= 0) return (int)hipErrorInvalidValue;
+  bytes[0] = (4 + (int64_t)ACC_N * n_blocks(a->R)) * 4;
+  bytes[1] = (int64_t)a->R * 3 * 4;
+  bytes[2] = (int64_t)a->R * 3 * 4;
+  bytes[3] = (int64_t)a->R * 4;
+  bytes[4] = (int64_t)a->R * 3 * 4;
+  return 0;
 }

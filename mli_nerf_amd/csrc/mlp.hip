@@ -609,6 +609,37 @@ extern "C" int mli_rgb_bwd(const mli_rgb_bwd_args* a, mli_stream_t s) {
   MLI_LAUNCH_CHECK();
 }
 
+extern "C" int mli_rgb_fwd_workspace(const mli_rgb_fwd_args* a, int64_t* bytes) {
+  const int64_t S = (int64_t)a->R * a->N;
+  if (S <= 0 || S % 256 != 0 || (a->n_heads != 1 && a->n_heads != 3)) return (int)hipErrorInvalidValue;
+  bytes[0] = S * 8 * 4;                                   // y
+  bytes[1] = S * 256 * 2;                                 // feat_frag
+  bytes[2] = (int64_t)MLI_HEAD_K0 * S * 2;                // x0T (training)
+  bytes[3] = (int64_t)a->n_heads * 4 * 256 * S * 2;       // xT (training)
+  bytes[4] = (int64_t)a->n_heads * 4 * (S / 32) * 64 * 16;  // masks (training)
+  return 0;
+}
+
+extern "C" int mli_rgb_bwd_workspace(const mli_rgb_bwd_args* a, int64_t* bytes) {
+  const int64_t S = (int64_t)a->R * a->N;
+  if (S <= 0 || S % 256 != 0) return (int)hipErrorInvalidValue;
+  bytes[0] = 3 * 4 * 256 * S * 2;  // dzT
+  bytes[1] = 3 * 4 * S * 2;        // dz4T
+  return 0;
+}
+
+extern "C" int mli_geo_bwd_workspace(const mli_geo_bwd_args* a, int64_t* bytes) {
+  const int64_t S = (int64_t)a->R * a->N;
+  if (S <= 0 || S % 256 != 0) return (int)hipErrorInvalidValue;
+  bytes[0] = 4 * 256 * S * 2;  // dzT
+  bytes[1] = 4 * S * 2;        // dz4T
+  bytes[2] = S * 4 * 4;        // d_nrm
+  bytes[3] = 256 * S * 2;      // dz1T
+  bytes[4] = S * 256 * 2;      // dh0_frag
+  bytes[5] = 0;
+  return 0;
+}
+
 extern "C" int mli_geo_bwd(const mli_geo_bwd_args* a, mli_stream_t s) {
   const int S = a->R * a->N;
   if (S % 256 != 0) return (int)hipErrorInvalidValue;

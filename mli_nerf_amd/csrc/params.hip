@@ -160,6 +160,11 @@ extern "C" int mli_pack(const mli_pack_args* a, mli_stream_t s) {
   MLI_LAUNCH_CHECK();
 }
 
+extern "C" int mli_pack_workspace(const mli_pack_args* a, int64_t* bytes) {
+  bytes[0] = (int64_t)(a->n_layers > 0 ? a->n_layers : 0) * 256 * 4;  // row_scale
+  return 0;
+}
+
 extern "C" int mli_grad_assemble(const mli_assemble_args* a, mli_stream_t s) {
   hipLaunchKernelGGL(assemble_kernel, dim3(256, a->n_layers), dim3(256), 0, (hipStream_t)s,
                      a->layers, a->inv_scale);

@@ -478,11 +478,22 @@ __global__ __launch_bounds__(CW * 64) void composite_bwd_geo_kernel(mli_composit
     *reinterpret_cast<f32x4*>(a.dz4 + 8 * s + 4) = o1;
   }
   dinv = wave_sum(dinv);
-  if (lane == 0) unsafeAtomicAdd(a.d_inv_s_acc, dinv);
+  if (lane == 0) a.d_inv_s_part[r] = dinv;
 }
 
-__global__ void svar_grad_kernel(mli_composite_bwd_geo_args a) {
-  a.d_s_var[0] = expf(a.s_var[0]) * a.d_inv_s_acc[0];  // inv_s = exp(s_var)
+// d s_var = exp(s_var) * sum_r d inv_s_r (inv_s = exp(s_var)); the per-ray partials summed in a
+// fixed order (strided per thread, then a fixed tree): bit-reproducible
+__global__ __launch_bounds__(256) void svar_grad_kernel(mli_composite_bwd_geo_args a) {
+  __shared__ float red[256];
+  float t = 0.f;
+  for (int r = threadIdx.x; r < a.R; r += 256) t += a.d_inv_s_part[r];
+  red[threadIdx.x] = t;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) a.d_s_var[0] = expf(a.s_var[0]) * red[0];
 }
 
 
@@ -572,9 +583,20 @@ extern "C" int mli_composite_bwd(const mli_composite_bwd_args* a, mli_stream_t s
 extern "C" int mli_composite_bwd_geo(const mli_composite_bwd_geo_args* a, mli_stream_t s) {
   if (a->R <= 0) return 0;
   if (a->N > 256) return (int)hipErrorInvalidValue;
+  if (a->d_inv_s_part == nullptr) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(composite_bwd_geo_kernel, dim3((a->R + CW - 1) / CW), dim3(CW * 64), 0, (hipStream_t)s, *a);
-  hipLaunchKernelGGL(svar_grad_kernel, dim3(1), dim3(1), 0, (hipStream_t)s, *a);
+  hipLaunchKernelGGL(svar_grad_kernel, dim3(1), dim3(256), 0, (hipStream_t)s, *a);
   MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_composite_bwd_geo_workspace(const mli_composite_bwd_geo_args* a, int64_t* bytes) {
+  if (a->R <= 0 || a->N <= 0) return (int)hipErrorInvalidValue;
+  const int64_t S = (int64_t)a->R * a->N;
+  bytes[0] = S * 8 * 4;   // dz4
+  bytes[1] = S * 4;       // d_sdf
+  bytes[2] = S * 3 * 4;   // d_grad
+  bytes[3] = (int64_t)a->R * 4;
+  return 0;
 }
 
 extern "C" int mli_ray_batch(const mli_ray_batch_args* a, mli_stream_t s) {

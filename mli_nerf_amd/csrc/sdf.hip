@@ -492,20 +492,24 @@ MLI_FI void field_points5(const float* center, const float* ray_unit, float d, i
 
 constexpr int LDS_SDFT_OFF = LDS_SDF;
 constexpr int LDS_DWS_OFF = LDS_SDF + MLI_SDF_T_PACK_BYTES;
-constexpr int LDS_SDF_BWD = LDS_DWS_OFF + 260 * 4;
+constexpr int LDS_SDF_BWD = LDS_DWS_OFF + MLP_WAVES * 260 * 4;  // one dW/db slice per wave
 
 // Per sample: d sdf_i of the 5 points, then per point: layer 0 recomputed from the FIELD
 // encoding (as field_mlp_kernel), dZ0 = (w_sdf ds_i [+ W1^T dZ1 for the center]) *
-// softplus'(z0), d enc = W0_enc^T dZ0 (MFMA), dW/db of linear_sdf by lane reductions.
+// softplus'(z0), d enc = W0_enc^T dZ0 (MFMA), dW/db of linear_sdf by lane reductions into the
+// wave's own LDS slice (plain adds: distinct lanes, distinct addresses), then the slices in
+// wave order into the workgroup's partial row and sdf_bwd_reduce_kernel over the workgroups in
+// order: no atomics, bit-reproducible.
 __global__ __launch_bounds__(MLP_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   load_block(lds, a.wsdf, PIECES);
   load_block(lds + LDS_SDFT_OFF, a.wsdf_t, SDFT_PIECES);
-  float* dws = reinterpret_cast<float*>(lds + LDS_DWS_OFF);
-  for (int i = threadIdx.x; i < 260; i += blockDim.x) dws[i] = 0.f;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* dws_all = reinterpret_cast<float*>(lds + LDS_DWS_OFF);
+  float* dws = dws_all + wave * 260;
+  for (int i = lane; i < 260; i += 64) dws[i] = 0.f;
   vm_wait(0);
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int S = a.R * a.N;
   const int tiles = S / 32;
@@ -567,7 +571,7 @@ __global__ __launch_bounds__(MLP_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_arg
       float t = (((ds[0] + ds[1]) + ds[2]) + ds[3]) + ds[4];
 #pragma unroll
       for (int o = 16; o > 0; o >>= 1) t += __shfl_xor(t, o);
-      if (c == 0) atomicAdd(&dws[256], t);
+      if (c == 0) dws[256] += t;
     }
     const half8* encp = reinterpret_cast<const half8*>(a.enc + (size_t)tile * TAPS * 8 * 512) + opaque_v(lane);
     const half8* dh0p = reinterpret_cast<const half8*>(a.dh0_frag + (size_t)tile * (16 * 64 * 8)) + lane;
@@ -639,7 +643,7 @@ __global__ __launch_bounds__(MLP_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_arg
           de[u] = mfma32(fr[(u * 16 + 1) * 64], z1, de[u]);
         }
         const float tot = half_reduce16(part, c);
-        if ((c & 1) == 0) atomicAdd(&dws[32 * t + acc_row((c >> 1) & 15, h)], tot);
+        if ((c & 1) == 0) dws[32 * t + acc_row((c >> 1) & 15, h)] += tot;
       }
       float* dst = a.d_enc + ((size_t)(tile * TAPS + pi) * 8) * 512 + lane * 8;
 #pragma unroll
@@ -657,9 +661,20 @@ __global__ __launch_bounds__(MLP_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_arg
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 257; i += blockDim.x) {
-    const float v = dws[i];
-    if (v != 0.f) unsafeAtomicAdd(i < 256 ? a.dw_sdf + i : a.db_sdf, v);
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < MLP_WAVES; ++w) v += dws_all[w * 260 + i];
+    a.partials[(size_t)blockIdx.x * 257 + i] = v;
   }
+}
+
+__global__ __launch_bounds__(320) void sdf_bwd_reduce_kernel(mli_sdf_bwd_args a, int blocks) {
+  const int i = threadIdx.x;
+  if (i >= 257) return;
+  float v = 0.f;
+  for (int b = 0; b < blocks; ++b) v += a.partials[(size_t)b * 257 + i];
+  if (i < 256) a.dw_sdf[i] = v;
+  else a.db_sdf[0] = v;
 }
 
 // Hash-grid backward, level-outer like encode5_kernel: lane (c, h) = sample c, level 2qq+h.
@@ -809,7 +824,13 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           if (i0 + u >= ntail) break;
-          if (v[u] != 0.0f) unsafeAtomicAdd(a.d_table + (size_t)slot[u] * 8 + (lane & 7), v[u]);
+          if (v[u] != 0.0f) {
+            if (a.deterministic)  // fixed point: integer sums are order-independent
+              atomicAdd(reinterpret_cast<unsigned long long*>(a.workspace) + (size_t)slot[u] * 8 + (lane & 7),
+                        (unsigned long long)__double2ll_rn((double)v[u] * 1099511627776.0));
+            else
+              unsafeAtomicAdd(a.d_table + (size_t)slot[u] * 8 + (lane & 7), v[u]);
+          }
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -861,6 +882,12 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
   }
 }
 
+
+// deterministic hash_bwd: d_table = float(fixed * 2^-40)
+__global__ __launch_bounds__(256) void fixed_to_float_kernel(const int64_t* w, float* out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    out[i] = (float)((double)w[i] * 9.094947017729282e-13);
+}
 
 // ================================================================ light visibility
 struct TraceArgs {
@@ -998,6 +1025,12 @@ extern "C" int mli_sdf(const mli_sdf_args* a, mli_stream_t s) {
   return 0;
 }
 
+extern "C" int mli_sdf_workspace(const mli_sdf_args* a, int64_t* bytes) {
+  const int64_t tiles = ((int64_t)a->R * a->n_per_ray + 31) / 32;
+  bytes[0] = a->mode == MLI_SDF_MODE_FIELD ? tiles * 32 * 640 * 2 : 0;  // enc
+  return 0;
+}
+
 extern "C" int mli_hashgrid_fwd(const mli_hashgrid_args* a, mli_stream_t s) {
   const int total = a->n * 16;
   if (total == 0) return 0;
@@ -1015,24 +1048,46 @@ extern "C" int mli_pack_sdf_t(const mli_pack_sdf_t_args* a, mli_stream_t s) {
   MLI_LAUNCH_CHECK();
 }
 
+inline int sdf_bwd_blocks(int S) { return S / 256 > 1024 ? 1024 : S / 256; }
+
 extern "C" int mli_sdf_bwd(const mli_sdf_bwd_args* a, mli_stream_t s) {
   const int S = a->R * a->N;
   if (S <= 0) return 0;
   if (S % 256 != 0 || !a->enc || !a->wsdf || !a->wsdf_t || !a->d_enc || !a->dz0_frag || !a->x0_rows ||
       !a->dw_sdf || !a->db_sdf || !a->dh0_frag || !a->d_nrm || !a->d_sdf || !a->d_grad)
     return (int)hipErrorInvalidValue;
-  int blocks = S / 256;
-  if (blocks > 1024) blocks = 1024;
+  if (!a->partials) return (int)hipErrorInvalidValue;
+  const int blocks = sdf_bwd_blocks(S);
   hipLaunchKernelGGL(sdf_bwd_kernel, dim3(blocks), dim3(MLP_WAVES * 64), LDS_SDF_BWD, (hipStream_t)s, *a);
+  hipLaunchKernelGGL(sdf_bwd_reduce_kernel, dim3(1), dim3(320), 0, (hipStream_t)s, *a, blocks);
   MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_sdf_bwd_workspace(const mli_sdf_bwd_args* a, int64_t* bytes) {
+  const int64_t S = (int64_t)a->R * a->N;
+  if (S <= 0 || S % 256 != 0) return (int)hipErrorInvalidValue;
+  bytes[0] = S * 640 * 4;                         // d_enc
+  bytes[1] = 5 * S * 256 * 2;                     // dz0_frag
+  bytes[2] = (int64_t)(3 + MLI_LEVELS * MLI_LEVEL_FEAT) * 5 * S * 2;  // x0_rows
+  bytes[3] = (int64_t)sdf_bwd_blocks((int)S) * 257 * 4;             // partials
+  return 0;
 }
 
 extern "C" int mli_hash_bwd(const mli_hash_bwd_args* a, mli_stream_t s) {
   const int S = a->R * a->N;
   if (S <= 0) return 0;
   if (S % 64 != 0 || !a->d_enc || !a->d_table) return (int)hipErrorInvalidValue;
+  if (a->deterministic && (!a->workspace || a->n_params <= 0)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(hash_bwd_kernel, dim3((S / 32 + 3) / 4), dim3(256), 0, (hipStream_t)s, *a);
+  if (a->deterministic)
+    hipLaunchKernelGGL(fixed_to_float_kernel, dim3(2048), dim3(256), 0, (hipStream_t)s, a->workspace, a->d_table,
+                       a->n_params);
   MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_hash_bwd_workspace(const mli_hash_bwd_args* a, int64_t* bytes) {
+  bytes[0] = a->deterministic ? a->n_params * 8 : 0;
+  return 0;
 }
 
 extern "C" int mli_light_visibility(const mli_light_visibility_args* a, mli_stream_t s) {
@@ -1057,4 +1112,14 @@ extern "C" int mli_light_visibility(const mli_light_visibility_args* a, mli_stre
   hipLaunchKernelGGL(trace_kernel, dim3(tb), dim3(256), LDS_SDF, st, tl);
   hipLaunchKernelGGL(light_finalize_kernel, dim3(rb), dim3(256), 0, st, *a, (const uint8_t*)a->visibility);
   MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_light_visibility_workspace(const mli_light_visibility_args* a, int64_t* bytes) {
+  const int64_t R = a->R;
+  bytes[0] = R * 3 * 4;  // light_unit
+  bytes[1] = R * 4;      // near_l
+  bytes[2] = R * 4;      // far_t
+  bytes[3] = R;          // inside
+  bytes[4] = R * 3 * 4;  // inter_pts
+  return 0;
 }

@@ -5,7 +5,8 @@
 // [rows][S] (samples contiguous), so the reduction axis (samples) is the contiguous one for
 // both MFMA operands: a plain NT GEMM.  Each workgroup owns a BM x BN output tile and a
 // k_split-sample slice; partial sums land in the fp32 outputs by atomics (few: one per
-// output element per slice).
+// output element per slice), or -- deterministic mode -- go to a per-slice partial slab that
+// wgrad_reduce_kernel sums in slice order.
 #include "common.h"
 
 #include <algorithm>
@@ -26,6 +27,8 @@ struct Job {
 struct KArgs {
   Job jobs[MAXJOBS];
   int n_jobs, S, k_split, n_split;
+  float* part;               // deterministic: per-job slabs [n_split][M*K + M], else NULL
+  int64_t part_base[MAXJOBS];
 };
 
 // Rows [t*ROWS, t*ROWS + ROWS) x BK samples from k, 8 x 16 B per row, rows clamped to n_rows.
@@ -131,6 +134,16 @@ __global__ __launch_bounds__(512) void wgrad_kernel(KArgs ka) {
     for (int d = 0; d < DEPTH; ++d)
       if (kk + d * BK < k1) step(d, kk + d * BK);
   }
+  // deterministic: this slice's partial tile into its slab (the reduce launch sums slices in
+  // order); else fp32 atomics into the caller-zeroed dw / db
+  float* slab = nullptr;
+  if (ka.part != nullptr) {
+    int jx = 0;
+#pragma unroll
+    for (int j = 1; j < MAXJOBS; ++j)
+      if (j < ka.n_jobs && bid >= ka.jobs[j].tile_base) jx = j;
+    slab = ka.part + ka.part_base[jx] + (int64_t)split * ((int64_t)J.M * J.K + J.M);
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -139,12 +152,50 @@ __global__ __launch_bounds__(512) void wgrad_kernel(KArgs ka) {
       for (int e = 0; e < 16; ++e) {
         const int row = tm * BM + wm * TM * 32 + i * 32 + acc_row(e, h);
         const int col = tn * BN + wn * TN * 32 + j * 32 + rl;
-        if (row < J.M && col < J.K) atomicAdd(J.dw + (size_t)row * J.ldw + col, acc[i][j][e]);
+        if (row < J.M && col < J.K) {
+          if (slab) slab[(size_t)row * J.K + col] = acc[i][j][e];
+          else atomicAdd(J.dw + (size_t)row * J.ldw + col, acc[i][j][e]);
+        }
       }
   if (do_bias) {
     bsum += __shfl_xor(bsum, 1);
     const int row = tm * BM + (tid >> 1);
-    if ((tid & 1) == 0 && (tid >> 1) < BM && row < J.M) atomicAdd(J.db + row, bsum);
+    if ((tid & 1) == 0 && (tid >> 1) < BM && row < J.M) {
+      if (slab) slab[(size_t)J.M * J.K + row] = bsum;
+      else atomicAdd(J.db + row, bsum);
+    }
+  }
+}
+
+// Deterministic mode: out = sum over slices 0..n_split-1 (in that order) of the partial slabs.
+// One thread per output element of every job (dW [M][K] then db [M]).
+struct RArgs {
+  const float* part;
+  int64_t base[MAXJOBS], first[MAXJOBS + 1];  // slab base / first global element of job j
+  float* dw[MAXJOBS];
+  float* db[MAXJOBS];
+  int M[MAXJOBS], K[MAXJOBS], ldw[MAXJOBS];
+  int n_jobs, n_split;
+};
+
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(RArgs r) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= r.first[r.n_jobs]) return;
+  int j = 0;
+#pragma unroll
+  for (int q = 1; q < MAXJOBS; ++q)
+    if (q < r.n_jobs && e >= r.first[q]) j = q;
+  const int64_t loc = e - r.first[j];
+  const int64_t MK = (int64_t)r.M[j] * r.K[j], stride = MK + r.M[j];
+  if (loc >= MK && r.db[j] == nullptr) return;
+  const float* p = r.part + r.base[j] + loc;
+  float acc = 0.f;
+  for (int sp = 0; sp < r.n_split; ++sp) acc += p[sp * stride];
+  if (loc < MK) {
+    const int row = (int)(loc / r.K[j]), col = (int)(loc - (int64_t)row * r.K[j]);
+    r.dw[j][(size_t)row * r.ldw[j] + col] = acc;
+  } else {
+    r.db[j][loc - MK] = acc;
   }
 }
 
@@ -185,32 +236,67 @@ inline int job_class(const mli_wgrad_job& j) {
 
 // One launch per class: tiles of all its jobs x n_split k-slices, n_split sized so the
 // grid holds about OCC workgroups per CU (OCC = resident 512-thread workgroups per CU).
-template <int BM, int BN, int WM, int WN, int OCC, int DEPTH>
-int launch(const mli_wgrad_args* a, int cls, hipStream_t s) {
-  KArgs ka;
+// plan(): the class's jobs and split (host only; also the workspace query); returns the
+// floats of partial slabs the deterministic mode needs, -1 on invalid jobs.
+template <int BM, int BN, int OCC>
+int64_t plan(const mli_wgrad_args* a, int cls, KArgs& ka) {
   ka.S = a->S;
   int n = 0, tiles = 0;
   for (int i = 0; i < a->n_jobs; ++i) {
     const mli_wgrad_job& j = a->jobs[i];
     if (job_class(j) != cls) continue;
-    if (n == MAXJOBS || j.ldw < j.K || j.M <= 0 || j.K <= 0) return (int)hipErrorInvalidValue;
+    if (n == MAXJOBS || j.ldw < j.K || j.M <= 0 || j.K <= 0) return -1;
     Job& J = ka.jobs[n++];
     J.a = j.a_rows; J.b = j.b_rows; J.M = j.M; J.K = j.K; J.ldw = j.ldw; J.dw = j.dw; J.db = j.db;
     J.tiles_n = (j.K + BN - 1) / BN;
     tiles += ((j.M + BM - 1) / BM) * J.tiles_n;
   }
   ka.n_jobs = n;
+  ka.part = nullptr;
   if (n == 0) return 0;
   const int want = std::max(1, 256 * OCC / tiles);
   const int steps = a->S / BK;
   ka.k_split = ((steps + want - 1) / want) * BK;
   ka.n_split = (a->S + ka.k_split - 1) / ka.k_split;
   int base = 0;
+  int64_t floats = 0;
   for (int i = 0; i < n; ++i) {
     ka.jobs[i].tile_base = base;
     base += ((ka.jobs[i].M + BM - 1) / BM) * ka.jobs[i].tiles_n * ka.n_split;
+    ka.part_base[i] = floats;
+    floats += (int64_t)ka.n_split * ((int64_t)ka.jobs[i].M * ka.jobs[i].K + ka.jobs[i].M);
   }
-  hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, DEPTH>), dim3(base), dim3(512), (BM + BN) * ROWB, s, ka);
+  return floats;
+}
+
+template <int BM, int BN, int WM, int WN, int OCC, int DEPTH>
+int launch(const mli_wgrad_args* a, int cls, hipStream_t s) {
+  KArgs ka;
+  const int64_t floats = plan<BM, BN, OCC>(a, cls, ka);
+  if (floats < 0) return (int)hipErrorInvalidValue;
+  if (ka.n_jobs == 0) return 0;
+  if (a->deterministic) {
+    if (a->workspace == nullptr) return (int)hipErrorInvalidValue;
+    ka.part = a->workspace;
+  }
+  int grid = 0;
+  for (int i = 0; i < ka.n_jobs; ++i) grid += ((ka.jobs[i].M + BM - 1) / BM) * ka.jobs[i].tiles_n * ka.n_split;
+  hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, DEPTH>), dim3(grid), dim3(512), (BM + BN) * ROWB, s, ka);
+  if (!a->deterministic) return (int)hipGetLastError();
+  RArgs r;
+  r.part = a->workspace;
+  r.n_jobs = ka.n_jobs;
+  r.n_split = ka.n_split;
+  int64_t first = 0;
+  for (int i = 0; i < ka.n_jobs; ++i) {
+    const Job& J = ka.jobs[i];
+    r.base[i] = ka.part_base[i];
+    r.first[i] = first;
+    r.dw[i] = J.dw; r.db[i] = J.db; r.M[i] = J.M; r.K[i] = J.K; r.ldw[i] = J.ldw;
+    first += (int64_t)J.M * J.K + J.M;
+  }
+  r.first[ka.n_jobs] = first;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((first + 255) / 256)), dim3(256), 0, s, r);
   return (int)hipGetLastError();
 }
 
@@ -223,6 +309,19 @@ extern "C" int mli_wgrad(const mli_wgrad_args* a, mli_stream_t s) {
   if (!e && (a->classes & CLS_WIDE)) e = launch<256, 320, 4, 2, 1, 1>(a, CLS_WIDE, (hipStream_t)s);
   if (!e && (a->classes & CLS_THIN)) e = launch<32, 256, 1, 8, 2, 2>(a, CLS_THIN, (hipStream_t)s);
   return e;
+}
+
+extern "C" int mli_wgrad_workspace(const mli_wgrad_args* a, int64_t* bytes) {
+  bytes[0] = 0;
+  if (a->S <= 0 || a->S % BK != 0) return (int)hipErrorInvalidValue;
+  if (!a->deterministic) return 0;
+  KArgs ka;
+  int64_t mx = 0, f;
+  if (a->classes & CLS_BIG) { if ((f = plan<256, 256, 1>(a, CLS_BIG, ka)) < 0) return (int)hipErrorInvalidValue; mx = std::max(mx, f); }
+  if (a->classes & CLS_WIDE) { if ((f = plan<256, 320, 1>(a, CLS_WIDE, ka)) < 0) return (int)hipErrorInvalidValue; mx = std::max(mx, f); }
+  if (a->classes & CLS_THIN) { if ((f = plan<32, 256, 2>(a, CLS_THIN, ka)) < 0) return (int)hipErrorInvalidValue; mx = std::max(mx, f); }
+  bytes[0] = mx * 4;
+  return 0;
 }
 
 extern "C" int mli_frag_rows(const mli_frag_rows_args* a, mli_stream_t s) {

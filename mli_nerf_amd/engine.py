@@ -87,6 +87,14 @@ class RenderEngine:
         self.u_fine = (C.c_float * 64)(*(layout.u_fine(cfg.n_fine) + [2.0] * (64 - cfg.n_fine)))
         self._pack_descs = None
         self.trace = None  # set to a list to record per-round sampler outputs (debug/tests)
+        # fixed-order reductions instead of fp32 atomics in mli_wgrad / mli_hash_bwd (ABI 8):
+        # bit-reproducible gradients at the cost of partial-slab traffic
+        self.deterministic = False
+        self._wplans = {}   # wgrad plans per buffer set (the prefetch lanes alternate)
+        # reference column -> packed k maps of the head layers (constant; uploaded once)
+        self._kinv = {(name, li): torch.from_numpy((layout.head_kinv(name, k_in) if li == 0 else
+                                                    np.arange(256)).astype(np.int16)).to(self.device)
+                      for name, k_in, _ in layout.HEADS for li in range(5)}
 
     # ------------------------------------------------------------------ parameters
     def set_normal_eps(self, normal_eps_value):
@@ -360,11 +368,15 @@ class RenderEngine:
         return sum(m * k + m for m, k in self._dw_sizes())
 
     def _wgrad_plan(self, dzT, dz4T, hd, dwbuf, flat, grad_out, S):
-        """Split-K jobs (host array) + device assemble descriptors; cached per buffer set."""
+        """Split-K jobs (host array) + device assemble descriptors; cached per buffer set (a
+        few: Trainer.prefetch alternates two engine lanes, each with its own buffers)."""
         key = (dzT.data_ptr(), dz4T.data_ptr(), hd["x0T"].data_ptr(), hd["xT"].data_ptr(), dwbuf.data_ptr(),
                flat.data_ptr(), grad_out.data_ptr(), S)
-        if getattr(self, "_wplan", None) is not None and self._wplan[0] == key:
-            return self._wplan[1], self._wplan[2]
+        hit = self._wplans.get(key)
+        if hit is not None:
+            return hit[0], hit[1]
+        if len(self._wplans) >= 8:
+            self._wplans.clear()
         sizes = self._dw_sizes()
         jobs, assemble, keep, off = [], [], [], 0
         for hdx, (name, k_in, k_out) in enumerate(layout.HEADS):
@@ -384,17 +396,28 @@ class RenderEngine:
                 v = self.param_view(flat, pre + ".weight_v")
                 g = self.param_view(flat, pre + ".weight_g")
                 k_ref = v.shape[1]
-                kinv = layout.head_kinv(name, k_ref) if li == 0 else np.arange(k_ref, dtype=np.int16)
-                kinv_t = torch.from_numpy(kinv.astype(np.int16)).to(self.device)
-                keep.append(kinv_t)
+                kinv_t = self._kinv[(name, li)]
                 assemble.append(L.AssembleLayer(L.ptr(dw), L.ptr(db), L.ptr(v), L.ptr(g), m, k_ref, k,
                                                 L.ptr(kinv_t), L.ptr(self.param_view(grad_out, pre + ".weight_v")),
                                                 L.ptr(self.param_view(grad_out, pre + ".weight_g")),
                                                 L.ptr(self.param_view(grad_out, pre + ".bias")), None))
         job_arr = (L.WgradJob * len(jobs))(*jobs)
         ad = _to_device_structs(assemble, self.device)
-        self._wplan = (key, job_arr, ad, keep)
+        self._wplans[key] = (job_arr, ad, keep)
         return job_arr, ad
+
+    def _wgrad(self, S, jobs, classes):
+        """mli_wgrad over `classes` (separate launches, timed separately); deterministic mode:
+        partial slabs in a workspace sized by mli_wgrad_workspace, else fp32 atomics into the
+        zeroed outputs (the caller zeroes them)."""
+        det = 1 if self.deterministic else 0
+        ws = None
+        if det:
+            q = L.WgradArgs(S, len(jobs), C.cast(jobs, C.c_void_p), sum(classes), 1, None)
+            nbytes = L.workspace("mli_wgrad", q)[0]
+            ws = self._buf("wgrad_ws", (max(nbytes, 4) // 4,))
+        for cls in classes:
+            L.call("mli_wgrad", L.WgradArgs(S, len(jobs), C.cast(jobs, C.c_void_p), cls, det, L.ptr(ws)))
 
     @torch.no_grad()
     def backward(self, st, d_rgb, d_o_r, d_o_s, d_o_re, flat, sdf_l1, grad_out):
@@ -418,10 +441,10 @@ class RenderEngine:
             self.gate_event = torch.cuda.Event()
             self.gate_event.record()
         dwbuf = self._buf("dw", (self._dw_total(),))
-        dwbuf.zero_()
+        if not self.deterministic:
+            dwbuf.zero_()
         jobs, ad = self._wgrad_plan(dzT, dz4T, hd, dwbuf, flat, grad_out, S)
-        for cls in (1, 2, 4):  # BIG, WIDE, THIN launch classes (timed separately)
-            L.call("mli_wgrad", L.WgradArgs(S, len(jobs), C.cast(jobs, C.c_void_p), cls))
+        self._wgrad(S, jobs, (1, 2, 4))  # BIG, WIDE, THIN launch classes
         L.call("mli_grad_assemble", L.AssembleArgs(15, L.ptr(ad), 1.0 / scale))
         return grad_out
 
@@ -506,8 +529,7 @@ class RenderEngine:
         scale = float(2.0 ** round(math.log2(max(R, 1)) + 2))
         f16 = torch.float16
         dz4, d_sdf, d_grad = self._buf("dz4", (N, R, 8)), self._buf("d_sdf", (N, R)), self._buf("d_grad", (N, R, 3))
-        dinv = self._buf("d_inv_s", (1,))
-        dinv.zero_()
+        dinv = self._buf("d_inv_s_part", (R,))
         anneal = min(progress / self.cfg.anneal_end, 1.0)
         s_var = self.param_view(flat, "s_var")
         L.call("mli_composite_bwd_geo", L.CompositeBwdGeoArgs(
@@ -525,17 +547,23 @@ class RenderEngine:
                                            L.ptr(dh0)))
         d_enc = self._buf("d_enc", (S * 640,))
         dz0f = self._buf("dz0_frag", (5 * S * 256,), f16)
-        b["dws"].zero_()
+        part = self._buf("sdf_bwd_part", (L.workspace("mli_sdf_bwd", L.SdfBwdArgs(R, N))[3] // 4,))
         L.call("mli_sdf_bwd", L.SdfBwdArgs(
             R, N, L.ptr(rays["center"]), L.ptr(rays["ray_unit"]), L.ptr(dists), L.ptr(rays["outside"]),
             L.ptr(fld["grad"]), L.ptr(fld["hess"]), L.ptr(d_sdf), L.ptr(d_grad), L.ptr(d_nrm), L.ptr(dh0),
             L.ptr(fld["enc"]), L.ptr(self.wsdf), L.ptr(self.wsdf_t), self.eps, self.grad_den, self.hess_den,
             float(w_eikonal), float(w_curvature), scale, L.ptr(d_enc), L.ptr(dz0f), L.ptr(b["x0_rows"]),
-            L.ptr(b["dws"][:256]), L.ptr(b["dws"][256:]), L.ptr(d_grad_ext), L.ptr(d_hess_ext)))
-        grad_table.zero_()
+            L.ptr(b["dws"][:256]), L.ptr(b["dws"][256:]), L.ptr(d_grad_ext), L.ptr(d_hess_ext), L.ptr(part)))
+        det = 1 if self.deterministic else 0
+        hws = None
+        if det:  # fixed-point accumulator (mli_hash_bwd_workspace), zeroed; d_table is overwritten
+            hws = self._buf("hash_ws", (grad_table.numel(),), torch.int64)
+            hws.zero_()
+        else:
+            grad_table.zero_()
         L.call("mli_hash_bwd", L.HashBwdArgs(R, N, L.ptr(rays["center"]), L.ptr(rays["ray_unit"]), L.ptr(dists),
                                              L.ptr(d_enc), self.levels, self.eps, int(self.active_levels),
-                                             L.ptr(grad_table)))
+                                             L.ptr(grad_table), det, L.ptr(hws), grad_table.numel()))
         # feature-major operand rows of the SDF weight gradients
         L.call("mli_frag_rows", L.FragRowsArgs(L.ptr(fld["h0"]), 16 * 512, T, 16, 1, L.ptr(b["h0_rows"]), S, 0, 0))
         for pi in range(5):
@@ -546,8 +574,9 @@ class RenderEngine:
                                               (256, 256), (256, layout.SDF_K0)])
         b["dw"] = self._buf("dw_a", (dw_total,))
         js, j5, ad, n_desc, _, _ = self._plan_a(b, flat, grad_flat, S)
-        b["dw"].zero_()
-        L.call("mli_wgrad", L.WgradArgs(S, len(js), C.cast(js, C.c_void_p), 7))
-        L.call("mli_wgrad", L.WgradArgs(5 * S, len(j5), C.cast(j5, C.c_void_p), 7))
+        if not self.deterministic:
+            b["dw"].zero_()
+        self._wgrad(S, js, (7,))
+        self._wgrad(5 * S, j5, (7,))
         L.call("mli_grad_assemble", L.AssembleArgs(n_desc, L.ptr(ad), 1.0 / scale))
         return grad_flat, grad_table

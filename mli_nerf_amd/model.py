@@ -252,6 +252,7 @@ class Model(torch.nn.Module):
         self.pipeline_chunks = True  # two inference chunks in flight (False: one stream)
         self._sdf_version = None
         self.image_width = self.image_size_train[1]
+        self.deterministic = False  # fixed-order gradient reductions (RenderEngine.deterministic)
 
     # -------------------------------------------------------------- parameter plumbing
     def _view(self, name, flat=None):
@@ -372,6 +373,7 @@ class Model(torch.nn.Module):
             self.engine = RenderEngine(self.pcfg, self.flat.device, self.stage)
         sdf = self.neural_sdf
         eng = self.engine
+        eng.deterministic = self.deterministic
         eng.set_normal_eps(sdf.normal_eps)
         eng.active_levels = int(sdf.active_levels)
         l0 = sdf.mlp.linears[0]

@@ -163,6 +163,9 @@ class Trainer:
         self.world_size = world_size
         if built:  # an injected model is already set up by its caller
             self._load_pre_trained(cfg)
+        # cfg.trainer.deterministic: fixed-order reductions instead of fp32 atomics in the
+        # split-K weight gradients and the hash-grid scatter (bit-reproducible steps)
+        model.deterministic = bool(cfg.trainer.get("deterministic", False))
         self.partial_grad_keywords = list(cfg.trainer.get("partial_grad", None) or [])
         self._set_requires_grad()
         self.weights = {k: v for k, v in cfg.trainer.loss_weight.items() if v}
@@ -415,8 +418,9 @@ class Trainer:
         N, R = dists.shape
         d_rgb, d_o_r = eng._buf("d_rgb", (R, 3)), eng._buf("d_o_r", (R, 3))
         d_o_s, d_o_re = eng._buf("d_o_s", (R, 1)), eng._buf("d_o_re", (R, 3))
-        if self._scratch is None or self._scratch.device != m.flat.device:
-            self._scratch = torch.zeros(16, device=m.flat.device)
+        n = L.workspace("mli_stage_b_loss", L.LossArgs(R, N))[0] // 4
+        if self._scratch is None or self._scratch.device != m.flat.device or self._scratch.numel() < n:
+            self._scratch = torch.empty(n, device=m.flat.device)
         w = self.weights
         intr = "intrinsic" in w
         L.call("mli_stage_b_loss", L.LossArgs(

@@ -66,7 +66,8 @@ def test_library_exports_header_entry_points():
     lib = L.lib()  # loads, binds argtypes and checks the ABI version
     assert lib.mli_abi_version() == L.ABI_VERSION
     fns = _declared_functions()
-    assert set(L.ENTRY_POINTS) | {"mli_abi_version", "mli_error_string"} == set(fns)
+    queries = {n + "_workspace" for n in L.WORKSPACE}
+    assert set(L.ENTRY_POINTS) | {"mli_abi_version", "mli_error_string"} | queries == set(fns)
     for name in fns:
         assert hasattr(lib, name), name
     assert lib.mli_error_string(0)
@@ -79,3 +80,46 @@ def test_product_path_does_not_import_oracle():
             if fn.endswith(".py"):
                 txt = open(os.path.join(dirpath, fn)).read()
                 assert not re.search(r"^\s*(from|import)\s+oracle", txt, re.M), fn
+
+
+def test_workspace_queries_match_engine_buffers():
+    """The host-only mli_<op>_workspace queries (no GPU call) give the byte sizes the engine
+    allocates for each op's scratch (mli_nerf_amd/engine.py), at the bench size."""
+    if not os.path.exists(L.LIB_PATH):
+        pytest.skip("libmli_hip.so not built")
+    from mli_nerf_amd import layout
+    R, N = 4096, 128
+    S = R * N
+    f16, f32 = 2, 4
+    assert L.workspace("mli_sdf", L.SdfArgs(1, R, N)) == [(S // 32) * 32 * 640 * f16]
+    assert L.workspace("mli_sdf", L.SdfArgs(0, R, 64)) == [0]
+    assert L.workspace("mli_rgb_fwd", L.RgbFwdArgs(R, N, n_heads=3)) == [
+        N * R * 8 * f32, S * 256 * f16, layout.K0 * S * f16, 3 * 4 * 256 * S * f16, 3 * 4 * (S // 32) * 64 * 4 * 4]
+    assert L.workspace("mli_rgb_bwd", L.RgbBwdArgs(R, N)) == [3 * 4 * 256 * S * f16, 3 * 4 * S * f16]
+    assert L.workspace("mli_geo_bwd", L.GeoBwdArgs(R, N)) == [
+        4 * 256 * S * f16, 4 * S * f16, N * R * 4 * f32, 256 * S * f16, S * 256 * f16, 0]
+    assert L.workspace("mli_composite_bwd_geo", L.CompositeBwdGeoArgs(R, N)) == [
+        N * R * 8 * f32, N * R * f32, N * R * 3 * f32, R * f32]
+    assert L.workspace("mli_sdf_bwd", L.SdfBwdArgs(R, N)) == [
+        S * 640 * f32, 5 * S * 256 * f16, layout.SDF_K0 * 5 * S * f16, 1024 * 257 * f32]
+    loss = L.workspace("mli_stage_b_loss", L.LossArgs(R, N))
+    assert loss[0] == (4 + 8 * (R // 256 + 256)) * f32 and loss[1:] == [R * 3 * f32, R * 3 * f32, R * f32, R * 3 * f32]
+    assert L.workspace("mli_light_visibility", L.LightVisibilityArgs(R)) == [R * 12, R * 4, R * 4, R, R * 12]
+    assert L.workspace("mli_pack", L.PackArgs(7)) == [7 * 256 * f32]
+    n_params = 45724048 * 8
+    assert L.workspace("mli_hash_bwd", L.HashBwdArgs(R, N, deterministic=1, n_params=n_params)) == [n_params * 8]
+    assert L.workspace("mli_hash_bwd", L.HashBwdArgs(R, N, n_params=n_params)) == [0]
+    # wgrad: the stage-b jobs (engine._wgrad_plan shapes): partial slabs only in deterministic mode
+    jobs = []
+    for name, k_in, k_out in layout.HEADS:
+        for m, k in [(256, layout.K0), (256, 256), (256, 256), (256, 256), (k_out, 256)]:
+            jobs.append(L.WgradJob(None, None, m, k, None, None, k))
+    arr = (L.WgradJob * len(jobs))(*jobs)
+    q = L.WgradArgs(S, len(jobs), C.cast(arr, C.c_void_p), 7, 0, None)
+    assert L.workspace("mli_wgrad", q) == [0]
+    q.deterministic = 1
+    ws = L.workspace("mli_wgrad", q)[0]
+    assert 16 * 2 ** 20 < ws < 512 * 2 ** 20, ws   # tens of MiB of fp32 partial slabs
+    q.S = 100   # not a multiple of the 64-sample k-step
+    with pytest.raises(RuntimeError):
+        L.workspace("mli_wgrad", q)
