@@ -375,6 +375,8 @@ class Trainer:
         return self._grad[:n], self._grad[n:]
 
     def _publish(self, lv):
+        """Step losses / PSNR as tensors of their own (the buffer tail is rewritten next step)."""
+        lv = lv.clone()
         self.losses = {k: lv[i] for i, k in enumerate(LOSS_NAMES) if k in self.weights}
         self.losses["total"] = lv[5]
         self.metrics["psnr"] = lv[6]

@@ -49,9 +49,15 @@ def _losses(tr, out, data):
 
 
 def test_reference_adamw_matches_fused_trainer():
-    """Both paths in deterministic mode: with fp32-atomic split-K sums the ~1e-7 run-to-run noise
-    of gradient elements below Adam's eps (|g| ~ 1e-9, eps 1e-8) flips their update by up to lr
-    between ANY two runs, so parameter equality at 1e-6 is only meaningful with fixed-order sums."""
+    """Both paths in deterministic mode (fixed-order split-K sums).  Step 0: the autograd
+    gradients on the named Parameters equal the fused step's flat gradient BITWISE (same
+    kernels, same loss derivatives).  The optimizers then differ by rounding only (torch's
+    lerp-form moments vs the fused kernel): parameters within 1e-6 for three steps.  Later a
+    weight whose fp32 value differs by ~1e-7 can round to a different fp16 value in the packed
+    MFMA weight image (a ~5e-4 relative jump), so the two trajectories drift apart slowly; over
+    5 steps the difference stays below 1e-3 of the update itself.  (With the default fp32-atomic
+    sums, gradient elements below Adam's eps flip between ANY two runs, so bitwise comparisons
+    need the deterministic mode.)"""
     it0 = 10000   # past the LR warm-up: the step uses lr = 1e-3
     cfg, ma = _model(deterministic=True)
     tra = Trainer(cfg, is_inference=False, model=ma)
@@ -63,6 +69,7 @@ def test_reference_adamw_matches_fused_trainer():
     lam = two_steps_with_warmup(it0, s.warm_up_end, tuple(s.two_steps), s.gamma)
     assert lam == 1.0   # LambdaLR factor stays 1 over the 5 steps (misc.py:43-52)
     opt = torch.optim.AdamW(mb.get_param_groups(o), lr=o.params.lr * lam, weight_decay=o.params.weight_decay)
+    p0 = mb.flat.detach().clone()
     for step in range(5):
         data, u = _batch(step)
         tra.train_step(data, u=u)
@@ -72,13 +79,18 @@ def test_reference_adamw_matches_fused_trainer():
         out = mb(data, u=u)
         total, _, _ = _losses(trb, out, data)
         total.backward()
+        if step == 0:
+            assert torch.equal(ma.flat.grad, mb.flat_grad_from_params())
+            assert float(tra.losses["total"]) == float(total)
         opt.step()
         opt.zero_grad(set_to_none=True)
+        diff = (ma.flat - mb.flat).abs().max().item()
+        if step < 3:
+            assert diff <= 1e-6, (step, diff)
     torch.cuda.synchronize()
-    diff = (ma.flat - mb.flat).abs().max().item()
-    moved = (ma.flat - _model()[1].flat).abs().max().item()
-    assert moved > 1e-3, moved      # the 5 steps did update the heads
-    assert diff <= 1e-6, diff
+    update = (mb.flat - p0).norm().item()
+    assert (mb.flat - p0).abs().max().item() > 1e-3        # the 5 steps did move the heads
+    assert (ma.flat - mb.flat).norm().item() <= 1e-3 * update
 
 
 def test_named_parameters_get_gradient_views():
