@@ -201,7 +201,7 @@ def test_end_to_end_forward_backward(case):
         {k: (v.cpu() if torch.is_tensor(v) else v) for k, v in out.items()}, data, pcfg)
     total_gpu = _gpu_total(out, to_dev(data), pcfg)
     total_gpu.backward()
-    g_flat = model.flat.grad.detach().cpu()
+    g_flat = model.flat_grad_from_params().cpu()   # the named Parameters' grads (views of one buffer)
     # oracle, unconditioned (its own sampler): forward agreement at the PSNR level
     sd16 = fp16_table_sd(sd)
     with torch.no_grad():
@@ -319,7 +319,7 @@ def test_fused_loss_step_matches_autograd_step(case):
     tr.current_iteration = 0
     tr.train_step_autograd(dd, u=u)
     auto = {k: float(v) for k, v in tr.losses.items()}
-    g_auto = model.flat.grad.detach().clone()
+    g_auto = model.flat_grad_from_params()
     print(case, "fused", fused, "autograd", auto)
     for k in auto:
         assert abs(fused[k] - auto[k]) <= 1e-5 * max(1.0, abs(auto[k])), k

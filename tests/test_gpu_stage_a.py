@@ -142,17 +142,17 @@ def test_stage_a_autograd_path_matches_fused():
     cfg, model, trainer, sd, data, u = _setup(64, 16, 4, 20000)
     batch = {k: v.to(DEV) for k, v in data.items()}
     trainer.compute_grads_a(batch, u=u.to(DEV))
-    g_fused, t_fused = trainer._grad.clone(), trainer._grad_table.clone()
+    g_fused, t_fused = trainer._grad[:model.flat.numel()].clone(), trainer._grad_table.clone()
     model.train()
     table = model.neural_sdf.tcnn_encoding.params
-    model.flat.grad = None
-    table.grad = None
+    for p in model.parameters():
+        p.grad = None
     out = model(batch, u=u.to(DEV))
     total, losses, _ = stage_b_losses(out, batch, trainer.weights)
     total.backward()
     torch.cuda.synchronize()
     for name, shape, off in model._layout_items():
         n = max(1, int(torch.tensor(shape).prod()))
-        a, b = model.flat.grad[off:off + n].cpu(), g_fused[off:off + n].cpu()
+        a, b = model.flat_grad_from_params()[off:off + n].cpu(), g_fused[off:off + n].cpu()
         assert _cos(a, b) > 0.99999 and float((a - b).norm() / b.norm().clamp_min(1e-30)) < 1e-3, name
     assert _cos(table.grad.cpu(), t_fused.cpu()) > 0.99999
