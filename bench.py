@@ -364,9 +364,10 @@ def main():
     ap.add_argument("--time-all-kernels", action="store_true",
                     help="train: HIP events around every launch (default: the MFMA kernels only; "
                          "each event pair costs GPU time between launches)")
-    ap.add_argument("--pipeline", choices=("off", "call", "heads", "wgrad"), default="off",
+    ap.add_argument("--pipeline", choices=("off", "call", "heads", "wgrad"), default="heads",
                     help="train: prefetch the next batch's geometry (sampling/FIELD) on a side stream, "
-                         "gated as Trainer.prefetch_gate; measured 13 %% slower than off (DESIGN §9)")
+                         "gated as Trainer.prefetch_gate (heads: after the heads forward of the step in "
+                         "flight); measured 4.77 vs 5.07 ms/step off (profiles/r2/s7)")
     ap.add_argument("--mode", choices=("train", "infer"), default="train",
                     help="train: BASELINE configs[1] step; infer: configs[4] full-frame render")
     ap.add_argument("--frames", type=int, default=4, help="infer: frames timed (after --warmup frames)")
