@@ -437,7 +437,7 @@ def main():
 
     # --pipeline: step k draws batch k+1 and issues its geometry (rays, sampling rounds, FIELD:
     # frozen SDF) on a side stream (Trainer.prefetch), and trains on batch k.  Every timed step
-    # still draws, samples, renders and trains one full batch.  Off by default: slower.
+    # still draws, samples, renders and trains one full batch.  On by default (gate heads).
     pipe = args.pipeline != "off" and model.stage == "b"
     cur = next_batch()
     if pipe:
@@ -461,9 +461,10 @@ def main():
     progress("warm-up done (%d steps)" % args.warmup)
     barrier()
     torch.cuda.synchronize()
-    if not args.no_kernel_timing:
+    names = None if args.time_all_kernels else {"mli_rgb_fwd", "mli_rgb_bwd", "mli_wgrad", "mli_sdf"}
+    if not args.no_kernel_timing and not pipe:
         L.PROFILE = []  # per-kernel HIP events on the launch stream, over the timed region
-        L.PROFILE_NAMES = None if args.time_all_kernels else {"mli_rgb_fwd", "mli_rgb_bwd", "mli_wgrad", "mli_sdf"}
+        L.PROFILE_NAMES = names
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -480,8 +481,19 @@ def main():
         elapsed = t.item()
     psnr = trainer.metrics["psnr"].item()
     loss = trainer.losses["total"].item()
+    k_steps = args.steps
+    if pipe and not args.no_kernel_timing:
+        # with the prefetch on, an event pair on one stream also times the other stream's
+        # kernels: the per-kernel table comes from extra (untimed) steps with the pipeline off
+        trainer.train_step(cur)          # retire the prefetched batch
+        k_steps = min(args.steps, 50)
+        L.PROFILE, L.PROFILE_NAMES = [], names
+        for _ in range(k_steps):
+            trainer.train_step(next_batch())
+        torch.cuda.synchronize()
+        prof, L.PROFILE = L.PROFILE, None
 
-    ktab, roof = kernel_table(prof, args.steps, R, N, args.fine, model.stage)
+    ktab, roof = kernel_table(prof, k_steps, R, N, args.fine, model.stage)
 
     step_ms = elapsed / args.steps * 1e3
     value = R * world * args.steps / elapsed
@@ -495,6 +507,8 @@ def main():
         "config": {"workload": "%s stage-%s train step" % (args.config, model.stage), "rays_per_gpu": R,
                    "samples_per_ray": N, "global_rays": R * world, "image": [Hh, W], "parallelism": "dp%d" % world,
                    "pipeline": ("geometry prefetch on a side stream, gate " + args.pipeline) if pipe else "off"},
+        "kernel_timing": ("HIP events on the launch stream over %d extra steps with the prefetch off" % k_steps)
+        if pipe else "HIP events on the launch stream over the timed steps",
         "psnr": round(psnr, 4), "loss": round(loss, 6),
         "roofline": roof, "kernels": ktab,
         "mfma_tflops_step": round(sum(kernel_flops(n, R, N, 64, args.fine, 4, model.stage) for n in ktab) /
