@@ -64,6 +64,9 @@ def kernel_flops(name, R, N, Nc, Nf, H, stage="b"):
         return 0
     if name == "mli_rgb_bwd":
         return 2 * S * sum(HIDDEN * o + 3 * HIDDEN * HIDDEN for o in HEAD_OUT)
+    if name == "mli_heads_bwd":    # algorithmic: the dX chain (as mli_rgb_bwd) + dW of the 256x256
+        # layers (as mli_wgrad BIG); the W3^T layer its layer-2 workgroups recompute is not counted
+        return kernel_flops("mli_rgb_bwd", R, N, Nc, Nf, H) + kernel_flops("mli_wgrad:big", R, N, Nc, Nf, H)
     if name == "mli_wgrad":
         return 2 * S * heads_fwd
     if name == "mli_wgrad:big":    # dW of the 256x256 hidden layers L1..L3 of the 3 heads
@@ -368,6 +371,11 @@ def main():
                     help="train: prefetch the next batch's geometry (sampling/FIELD) on a side stream, "
                          "gated as Trainer.prefetch_gate (heads: after the heads forward of the step in "
                          "flight); measured 4.77 vs 5.07 ms/step off (profiles/r2/s7)")
+    ap.add_argument("--heads-bwd", choices=("fused", "split"), default="fused",
+                    help="stage-b heads backward: fused (mli_heads_bwd: dX chain + 256x256 dW in one launch) "
+                         "or split (mli_rgb_bwd + mli_wgrad BIG)")
+    ap.add_argument("--heads-split", default="0,0,0",
+                    help="mli_heads_bwd workgroups per (head, layer 1..3), 0 = library default")
     ap.add_argument("--mode", choices=("train", "infer"), default="train",
                     help="train: BASELINE configs[1] step; infer: configs[4] full-frame render")
     ap.add_argument("--frames", type=int, default=4, help="infer: frames timed (after --warmup frames)")
@@ -407,6 +415,8 @@ def main():
     model.load_state_dict(synthetic.make_state_dict(log2T=22, seed=0, heads="rgb" if stage_a else "rgb_r_s"))
     model = model.to(dev)
     trainer = Trainer(cfg, is_inference=False, model=model, world_size=world)
+    model.heads_bwd = args.heads_bwd
+    model.heads_split = tuple(int(x) for x in args.heads_split.split(","))
     if stage_a:
         # steady state of stage a: past the coarse-to-fine ramp (all 16 levels active)
         trainer.current_iteration = args.iteration
@@ -461,7 +471,7 @@ def main():
     progress("warm-up done (%d steps)" % args.warmup)
     barrier()
     torch.cuda.synchronize()
-    names = None if args.time_all_kernels else {"mli_rgb_fwd", "mli_rgb_bwd", "mli_wgrad", "mli_sdf"}
+    names = None if args.time_all_kernels else {"mli_rgb_fwd", "mli_rgb_bwd", "mli_heads_bwd", "mli_wgrad", "mli_sdf"}
     if not args.no_kernel_timing and not pipe:
         L.PROFILE = []  # per-kernel HIP events on the launch stream, over the timed region
         L.PROFILE_NAMES = names
@@ -506,7 +516,8 @@ def main():
         "data": "synthetic (seeded cameras/lights/labels, random-init weights, full 2^22 hash table)",
         "config": {"workload": "%s stage-%s train step" % (args.config, model.stage), "rays_per_gpu": R,
                    "samples_per_ray": N, "global_rays": R * world, "image": [Hh, W], "parallelism": "dp%d" % world,
-                   "pipeline": ("geometry prefetch on a side stream, gate " + args.pipeline) if pipe else "off"},
+                   "pipeline": ("geometry prefetch on a side stream, gate " + args.pipeline) if pipe else "off",
+                   "heads_bwd": args.heads_bwd},
         "kernel_timing": ("HIP events on the launch stream over %d extra steps with the prefetch off" % k_steps)
         if pipe else "HIP events on the launch stream over the timed steps",
         "psnr": round(psnr, 4), "loss": round(loss, 6),

@@ -72,6 +72,12 @@ class RgbBwdArgs(C.Structure):
                 ("dz4T", P)]
 
 
+class HeadsBwdArgs(C.Structure):
+    _fields_ = [("R", I32), ("N", I32), ("dz4", P), ("wbwd", P), ("masks", P), ("xT", P), ("dz0T", P),
+                ("dz4T", P), ("dw", P * 9), ("db", P * 9), ("split", I32 * 3), ("deterministic", I32),
+                ("workspace", P)]
+
+
 class WgradJob(C.Structure):
     _fields_ = [("a_rows", P), ("b_rows", P), ("M", I32), ("K", I32), ("dw", P), ("db", P), ("ldw", I32)]
 
@@ -174,13 +180,14 @@ class FragRowsArgs(C.Structure):
                 ("ld", I64), ("col0", I64), ("row0", I32)]
 
 
-ABI_VERSION = 8  # include/mli_hip.h MLI_ABI_VERSION
+ABI_VERSION = 9  # include/mli_hip.h MLI_ABI_VERSION
 
 ENTRY_POINTS = {
     "mli_rays": RaysArgs, "mli_hashgrid_fwd": HashgridArgs, "mli_sdf": SdfArgs,
     "mli_sample_coarse": SampleCoarseArgs, "mli_sample_fine": SampleFineArgs,
     "mli_rgb_fwd": RgbFwdArgs, "mli_composite_fwd": CompositeArgs,
-    "mli_composite_bwd": CompositeBwdArgs, "mli_rgb_bwd": RgbBwdArgs, "mli_wgrad": WgradArgs,
+    "mli_composite_bwd": CompositeBwdArgs, "mli_rgb_bwd": RgbBwdArgs, "mli_heads_bwd": HeadsBwdArgs,
+    "mli_wgrad": WgradArgs,
     "mli_pack": PackArgs, "mli_pack_sdf": PackSdfArgs, "mli_grad_assemble": AssembleArgs,
     "mli_adamw": AdamwArgs, "mli_cast_f16": CastArgs, "mli_stage_b_loss": LossArgs,
     "mli_composite_bwd_geo": CompositeBwdGeoArgs, "mli_geo_bwd": GeoBwdArgs, "mli_sdf_bwd": SdfBwdArgs,
@@ -193,7 +200,7 @@ ENTRY_POINTS = {
 WORKSPACE = {
     "mli_sdf": 1, "mli_rgb_fwd": 5, "mli_rgb_bwd": 2, "mli_wgrad": 1, "mli_composite_bwd_geo": 4,
     "mli_geo_bwd": 6, "mli_sdf_bwd": 4, "mli_hash_bwd": 1, "mli_light_visibility": 5, "mli_stage_b_loss": 5,
-    "mli_pack": 1,
+    "mli_pack": 1, "mli_heads_bwd": 3,
 }
 
 _lib = None

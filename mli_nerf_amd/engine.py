@@ -87,9 +87,15 @@ class RenderEngine:
         self.u_fine = (C.c_float * 64)(*(layout.u_fine(cfg.n_fine) + [2.0] * (64 - cfg.n_fine)))
         self._pack_descs = None
         self.trace = None  # set to a list to record per-round sampler outputs (debug/tests)
-        # fixed-order reductions instead of fp32 atomics in mli_wgrad / mli_hash_bwd (ABI 8):
+        # fixed-order reductions instead of fp32 atomics in mli_wgrad / mli_heads_bwd /
+        # mli_hash_bwd:
         # bit-reproducible gradients at the cost of partial-slab traffic
         self.deterministic = False
+        # stage-b heads backward: "fused" = mli_heads_bwd (dX chain + the 256x256 dW in one
+        # launch, dZ_1..3 stay on chip) + the WIDE/THIN dW; "split" = mli_rgb_bwd + mli_wgrad
+        # BIG/WIDE/THIN (dZ_0..3 through HBM)
+        self.heads_bwd = "fused"
+        self.heads_split = (0, 0, 0)  # mli_heads_bwd workgroups per (head, layer 1..3); 0 = default
         self._wplans = {}   # wgrad plans per buffer set (the prefetch lanes alternate)
         # reference column -> packed k maps of the head layers (constant; uploaded once)
         self._kinv = {(name, li): torch.from_numpy((layout.head_kinv(name, k_in) if li == 0 else
@@ -367,18 +373,20 @@ class RenderEngine:
     def _dw_total(self):
         return sum(m * k + m for m, k in self._dw_sizes())
 
-    def _wgrad_plan(self, dzT, dz4T, hd, dwbuf, flat, grad_out, S):
-        """Split-K jobs (host array) + device assemble descriptors; cached per buffer set (a
-        few: Trainer.prefetch alternates two engine lanes, each with its own buffers)."""
-        key = (dzT.data_ptr(), dz4T.data_ptr(), hd["x0T"].data_ptr(), hd["xT"].data_ptr(), dwbuf.data_ptr(),
-               flat.data_ptr(), grad_out.data_ptr(), S)
+    def _wgrad_plan(self, dz_rows, dz4T, hd, dwbuf, flat, grad_out, S):
+        """Split-K jobs (host array) + device assemble descriptors + the fused kernel's dW / db
+        pointers (layers 1..3); cached per buffer set (a few: Trainer.prefetch alternates two
+        engine lanes, each with its own buffers).  dz_rows(hdx, li): the dZ_li rows [256][S]."""
+        key = (dz_rows(0, 0).data_ptr(), dz4T.data_ptr(), hd["x0T"].data_ptr(), hd["xT"].data_ptr(),
+               dwbuf.data_ptr(), flat.data_ptr(), grad_out.data_ptr(), S)
         hit = self._wplans.get(key)
         if hit is not None:
-            return hit[0], hit[1]
+            return hit[0], hit[1], hit[2]
         if len(self._wplans) >= 8:
             self._wplans.clear()
         sizes = self._dw_sizes()
-        jobs, assemble, keep, off = [], [], [], 0
+        jobs, assemble, off = [], [], 0
+        fused_dw, fused_db = [0] * 9, [0] * 9
         for hdx, (name, k_in, k_out) in enumerate(layout.HEADS):
             for li in range(5):
                 m, k = sizes[hdx * 5 + li]
@@ -386,9 +394,10 @@ class RenderEngine:
                 db = dwbuf[off + m * k:off + m * k + m]
                 off += m * k + m
                 if li == 0:
-                    a_rows, b_rows = dzT[hdx, 0], hd["x0T"]
+                    a_rows, b_rows = dz_rows(hdx, 0), hd["x0T"]
                 elif li < 4:
-                    a_rows, b_rows = dzT[hdx, li], hd["xT"][hdx, li - 1]
+                    a_rows, b_rows = dz_rows(hdx, li), hd["xT"][hdx, li - 1]
+                    fused_dw[hdx * 3 + li - 1], fused_db[hdx * 3 + li - 1] = L.ptr(dw), L.ptr(db)
                 else:
                     a_rows, b_rows = dz4T[hdx], hd["xT"][hdx, 3]
                 jobs.append(L.WgradJob(L.ptr(a_rows), L.ptr(b_rows), m, k, L.ptr(dw), L.ptr(db), k))
@@ -403,8 +412,9 @@ class RenderEngine:
                                                 L.ptr(self.param_view(grad_out, pre + ".bias")), None))
         job_arr = (L.WgradJob * len(jobs))(*jobs)
         ad = _to_device_structs(assemble, self.device)
-        self._wplans[key] = (job_arr, ad, keep)
-        return job_arr, ad
+        ptrs = ((C.c_void_p * 9)(*fused_dw), (C.c_void_p * 9)(*fused_db))
+        self._wplans[key] = (job_arr, ad, ptrs)
+        return job_arr, ad, ptrs
 
     def _wgrad(self, S, jobs, classes):
         """mli_wgrad over `classes` (separate launches, timed separately); deterministic mode:
@@ -432,19 +442,33 @@ class RenderEngine:
                                                        L.ptr(comp["o_r"]), L.ptr(comp["o_s"]), L.ptr(c(d_rgb)),
                                                        L.ptr(c(d_o_r)), L.ptr(c(d_o_s)), L.ptr(c(d_o_re)),
                                                        scale, L.ptr(dz4)))
-        dzT = self._buf("dzT", (3, 4, 256, S), torch.float16)
         dz4T = self._buf("dz4T", (3, 4, S), torch.float16)
-        L.call("mli_rgb_bwd", L.RgbBwdArgs(R, N, L.ptr(dz4), L.ptr(self.wbwd), L.ptr(hd["masks"]), L.ptr(dzT),
-                                           L.ptr(dz4T)))
-        # weight gradients (packed-k space), zeroed then accumulated by split-K atomics
+        dwbuf = self._buf("dw", (self._dw_total(),))
+        if not self.deterministic:
+            dwbuf.zero_()  # split-K partials add into it (fp32 atomics)
+        if self.heads_bwd == "fused":
+            # dX chain + dW of the 256x256 layers in one launch; it writes dZ_0 and dz4 rows for
+            # the layer-0 (WIDE) and layer-4 (THIN) dW
+            dz0T = self._buf("dz0T", (3, 256, S), torch.float16)
+            jobs, ad, (pdw, pdb) = self._wgrad_plan(lambda h, li: dz0T[h], dz4T, hd, dwbuf, flat, grad_out, S)
+            args = L.HeadsBwdArgs(R, N, L.ptr(dz4), L.ptr(self.wbwd), L.ptr(hd["masks"]), L.ptr(hd["xT"]),
+                                  L.ptr(dz0T), L.ptr(dz4T), pdw, pdb, (C.c_int * 3)(*self.heads_split),
+                                  1 if self.deterministic else 0, None)
+            if self.deterministic:
+                nbytes = L.workspace("mli_heads_bwd", args)[2]
+                args.workspace = L.ptr(self._buf("heads_ws", (max(nbytes, 4) // 4,)))
+            L.call("mli_heads_bwd", args)
+            classes = (2, 4)  # WIDE, THIN
+        else:
+            dzT = self._buf("dzT", (3, 4, 256, S), torch.float16)
+            L.call("mli_rgb_bwd", L.RgbBwdArgs(R, N, L.ptr(dz4), L.ptr(self.wbwd), L.ptr(hd["masks"]), L.ptr(dzT),
+                                               L.ptr(dz4T)))
+            jobs, ad, _ = self._wgrad_plan(lambda h, li: dzT[h, li], dz4T, hd, dwbuf, flat, grad_out, S)
+            classes = (1, 2, 4)  # BIG, WIDE, THIN launch classes
         if self.gate_wgrad:  # Trainer.prefetch(gate="wgrad"): next geometry may start here
             self.gate_event = torch.cuda.Event()
             self.gate_event.record()
-        dwbuf = self._buf("dw", (self._dw_total(),))
-        if not self.deterministic:
-            dwbuf.zero_()
-        jobs, ad = self._wgrad_plan(dzT, dz4T, hd, dwbuf, flat, grad_out, S)
-        self._wgrad(S, jobs, (1, 2, 4))  # BIG, WIDE, THIN launch classes
+        self._wgrad(S, jobs, classes)
         L.call("mli_grad_assemble", L.AssembleArgs(15, L.ptr(ad), 1.0 / scale))
         return grad_out
 
