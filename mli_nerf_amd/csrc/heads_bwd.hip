@@ -209,10 +209,11 @@ MLI_FI f32x16 masked(const f32x16& acc, const u32x4& mv, int t) {
   return v;
 }
 
-// acc = W^T chunk (32 x 256) x IN (256 x 32 samples)
-// (loads bounded: a compiler memory fence every PF k-steps keeps the LDS reads from all being
-// hoisted to the top of the phase -- at one wave per SIMD the registers hold the dW tile)
-constexpr int PF = 2;
+// acc = W^T chunk (32 x 256) x IN (256 x 32 samples).  At one wave per SIMD nothing hides an
+// LDS read's latency but the wave's own MFMAs: the 16 A fragments are read in groups of PF,
+// group g+1 issued before the MFMAs of group g (the fence keeps the compiler from hoisting all
+// 16 reads to the top, which costs 64 registers the dW tile needs).
+constexpr int PF = 4;
 MLI_FI void ld_fence() { asm volatile("" ::: "memory"); }
 // x redefined here (after the stores before it): what consumes x is not hoisted above
 MLI_FI void opaque_h8(half8& x) { asm volatile("" : "+v"(x)::"memory"); }
@@ -220,10 +221,18 @@ MLI_FI void opaque_h8(half8& x) { asm volatile("" : "+v"(x)::"memory"); }
 MLI_FI f32x16 chunk16(const uint8_t* chunk, const half8* in, int lane) {
   f32x16 acc = zero16();
   const half8* w = reinterpret_cast<const half8*>(chunk) + lane;
+  half8 buf[2][PF];
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    if (q % PF == 0) ld_fence();
-    acc = mfma32(w[q * 64], in[q], acc);
+  for (int i = 0; i < PF; ++i) buf[0][i] = w[i * 64];
+#pragma unroll
+  for (int g = 0; g < 16 / PF; ++g) {
+    if (g + 1 < 16 / PF) {
+#pragma unroll
+      for (int i = 0; i < PF; ++i) buf[(g + 1) & 1][i] = w[((g + 1) * PF + i) * 64];
+    }
+    ld_fence();
+#pragma unroll
+    for (int i = 0; i < PF; ++i) acc = mfma32(buf[g & 1][i], in[g * PF + i], acc);
   }
   return acc;
 }
@@ -287,17 +296,27 @@ template <bool XREG>
 MLI_FI void dw_tile(f32x16 (&acc)[2], const uint8_t* zb, const uint8_t* xs, const half8 (&xr)[2][8], const Ctx& k,
                     bool do_bias, float& bp) {
   const int r = k.c, sw = swz(k.c);
-  auto xf = [&](int cb, int q) MLI_LAMBDA_FI {
-    return XREG ? xr[cb][q]
-                : *reinterpret_cast<const half8*>(xs + (32 * cb + r) * 256 + (((8 * k.h + q) ^ sw) << 4));
-  };
+  // operands of k-steps q, q+1: 2 dZ^T fragments + 4 X fragments (X: registers or the slice)
+  struct Ops { half8 a[2], x[4]; };
+  auto load = [&](Ops& o, int q) MLI_LAMBDA_FI {
 #pragma unroll
-  for (int q = 0; q < 8; q += 2) {
-    if (q % 4 == 0) ld_fence();
-    const half8 a0 = *reinterpret_cast<const half8*>(zb + r * SROW + (64 * k.h + 8 * q) * 2);
-    const half8 a1 = *reinterpret_cast<const half8*>(zb + r * SROW + (64 * k.h + 8 * q + 8) * 2);
-    if (do_bias) bp += hsum8(a0) + hsum8(a1);
-    dw_mma4(acc[0], acc[1], a0, a1, xf(0, q), xf(0, q + 1), xf(1, q), xf(1, q + 1));
+    for (int u = 0; u < 2; ++u) o.a[u] = *reinterpret_cast<const half8*>(zb + r * SROW + (64 * k.h + 8 * (q + u)) * 2);
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        o.x[2 * cb + u] = XREG ? xr[cb][q + u]
+                               : *reinterpret_cast<const half8*>(xs + (32 * cb + r) * 256 + (((8 * k.h + q + u) ^ sw) << 4));
+  };
+  Ops ops[2];
+  load(ops[0], 0);
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    if (g + 1 < 4) load(ops[(g + 1) & 1], 2 * g + 2);
+    ld_fence();
+    const Ops& o = ops[g & 1];
+    if (do_bias) bp += hsum8(o.a[0]) + hsum8(o.a[1]);
+    dw_mma4(acc[0], acc[1], o.a[0], o.a[1], o.x[0], o.x[1], o.x[2], o.x[3]);
   }
 }
 
@@ -334,11 +353,15 @@ MLI_FI u32x4 mask_read(const uint8_t* slot, const Ctx& k) {
   return *reinterpret_cast<const u32x4*>(slot + k.wave * 1024 + k.lane * 16);
 }
 
-// W4^T (resident) x dz4 -> dZ_3 n-tile t, masked
+// W4^T (resident) x dz4 -> dZ_3 n-tile t, masked; the 8 fragments read up front
 template <int L>
-MLI_FI f32x16 w4_tile(const Ctx& k, const half8& z, const u32x4& mv, int t) {
+MLI_FI void w4_frags(half8 (&w)[8], const Ctx& k) {
   constexpr Map M = map_of(L);
-  const half8 w = reinterpret_cast<const half8*>(k.lds + M.w4 + t * 1024)[k.lane];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) w[t] = reinterpret_cast<const half8*>(k.lds + M.w4 + t * 1024)[k.lane];
+}
+
+MLI_FI f32x16 w4_tile(const half8& w, const half8& z, const u32x4& mv, int t) {
   return masked(mfma32(w, z, zero16()), mv, t);
 }
 
@@ -426,10 +449,11 @@ MLI_FI void body1(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
     {
       const half8 z = z4_frag<L>(k);
       const u32x4 mv = mask_read(k.lds + M.mask + 3 * MASKB, k);
-      half8 zz = z;
+      half8 zz = z, w4[8];
+      w4_frags<L>(w4, k);
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
-        const f32x16 v = w4_tile<L>(k, zz, mv, t);
+        const f32x16 v = w4_tile(w4[t], zz, mv, t);
         A[2 * t] = acc_to_frag(v, 0);
         A[2 * t + 1] = acc_to_frag(v, 1);
         opaque_h8(zz);
@@ -458,11 +482,14 @@ MLI_FI void body1(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         if (ROLE == RING) ring_issue<L, 24>(rg, k);
+        // dW of the previous n-tile, then this n-tile's chain step: kept apart (sched_barrier)
+        // so their operand registers are not live together
+        if (t > 0) dw_tile<false>(dw[t - 1], zt0 + ((t - 1) & 1) * ZT, xs, xr_unused, k, bias_w[t - 1], bp[(t - 1) >> 2]);
+        __builtin_amdgcn_sched_barrier(0);
         const f32x16 v = masked(chunk16(k.lds + M.ring + (cur % NSLOT) * WCH, B, k.lane), mv, t);
         A[2 * t] = acc_to_frag(v, 0);
         A[2 * t + 1] = acc_to_frag(v, 1);
         stage(zt0 + (t & 1) * ZT, v, k);
-        if (t > 0) dw_tile<false>(dw[t - 1], zt0 + ((t - 1) & 1) * ZT, xs, xr_unused, k, bias_w[t - 1], bp[(t - 1) >> 2]);
         if (ROLE == RING) vm_wait63(RING_OPS * (DIST - 1));
         if (ROLE == LOAD && t == 7) vm_wait63(0);
         block_sync();
@@ -548,10 +575,11 @@ MLI_FI void body2(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
     {
       const half8 z = z4_frag<L>(k);
       const u32x4 mv = mask_read(k.lds + M.mask + 3 * MASKB, k);
-      half8 zz = z;
+      half8 zz = z, w4[8];
+      w4_frags<L>(w4, k);
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
-        const f32x16 v = w4_tile<L>(k, zz, mv, t);
+        const f32x16 v = w4_tile(w4[t], zz, mv, t);
         A[2 * t] = acc_to_frag(v, 0);
         A[2 * t + 1] = acc_to_frag(v, 1);
         opaque_h8(zz);
@@ -569,9 +597,10 @@ MLI_FI void body2(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
         mask_dma<L>(k, k.a->masks, 3, Tn, 3, lw);
         mask_dma<L>(k, k.a->masks, 2, Tn, par ^ 1, lw);
       }
+      if (t > 0) dw_tile<true>(dw[t - 1], zt0 + ((t - 1) & 1) * ZT, nullptr, xr, k, bias_w[t - 1], bp[(t - 1) >> 2]);
+      __builtin_amdgcn_sched_barrier(0);
       const f32x16 v = masked(chunk16(k.lds + M.ring + (cur % NSLOT) * WCH, A, k.lane), mv, t);
       stage(zt0 + (t & 1) * ZT, v, k);
-      if (t > 0) dw_tile<true>(dw[t - 1], zt0 + ((t - 1) & 1) * ZT, nullptr, xr, k, bias_w[t - 1], bp[(t - 1) >> 2]);
       if (ROLE == RING) vm_wait63(RING_OPS * (DIST - 1));
       if (ROLE == LOAD && t == 7) vm_wait63(0);
       block_sync();
@@ -620,16 +649,22 @@ MLI_FI void body3(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
     {
       const half8 z = z4_frag<L>(k);
       if (k.h == 0) {
+        // the rows from the fp32 values (a bit_cast of a vector element can yield element 0)
+        const float* zs = reinterpret_cast<const float*>(k.lds + M.z4 + k.wave * 3 * 256) + k.lane;
         const int m = T * TILE + k.wave * 32 + k.c;
 #pragma unroll
         for (int j = 0; j < 3; ++j)
-          if (j < no) k.a->dz4T[((size_t)k.hd * 4 + j) * k.S + m] = __builtin_bit_cast(uint16_t, z[j]);
+          if (j < no) {
+            const f16 zj = (f16)zs[j * 64];
+            k.a->dz4T[((size_t)k.hd * 4 + j) * k.S + m] = __builtin_bit_cast(uint16_t, zj);
+          }
       }
       const u32x4 mv = mask_read(k.lds + M.mask, k);
-      half8 zz = z;
+      half8 zz = z, w4[8];
+      w4_frags<L>(w4, k);
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
-        stage(img + t * ZT, w4_tile<L>(k, zz, mv, t), k);
+        stage(img + t * ZT, w4_tile(w4[t], zz, mv, t), k);
         opaque_h8(zz);
       }
     }

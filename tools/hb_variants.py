@@ -1,0 +1,91 @@
+"""Knock-out variants of the fused heads backward (experiment tooling, not the product).
+
+Builds libmli_hip.so variants into xlib/ from text patches of mli_nerf_amd/csrc/heads_bwd.hip
+(the product source stays free of experiment branches), then -- on the GPU box -- times
+mli_heads_bwd in bench.py with each (MLI_HIP_LIB=...).
+
+    python tools/hb_variants.py build [names...]     # here (hipcc cross-compiles)
+    python tools/hb_variants.py run [names...]       # on the GPU box (gpurun)
+"""
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, REPO)
+from mli_nerf_amd import build as B  # noqa: E402
+
+SRC = "heads_bwd.hip"
+
+# name -> list of (old, new) text patches of heads_bwd.hip
+VARIANTS = {
+    "base": [],
+    # no dW MFMAs: the chain, DMA and staging alone
+    "no_dw": [('  asm("s_nop 1\\n\\t"\n      "v_mfma_f32_32x32x16_f16 %0, %2, %4, %0\\n\\t"',
+               '  if (0) asm("s_nop 1\\n\\t"\n      "v_mfma_f32_32x32x16_f16 %0, %2, %4, %0\\n\\t"')],
+    # no chain MFMAs (zeros): DMA, staging and dW
+    "no_chain": [("  for (int q = 0; q < 16; ++q) {\n    if (q % PF == 0) ld_fence();\n    acc = mfma32(w[q * 64], in[q], acc);",
+                  "  for (int q = 0; q < 16; ++q) {\n    if (q % PF == 0) ld_fence();\n    if (q == 99) acc = mfma32(w[q * 64], in[q], acc);")],
+    # the RING waves do not wait for the next weight chunk (wrong results; latency probe)
+    "no_ringwait": [("        if (ROLE == RING) vm_wait63(RING_OPS * (DIST - 1));",
+                     "        if (ROLE == RING) {}")],
+    # no s_barrier in the phase loop (wrong results; synchronisation probe)
+    "no_barrier": [("        block_sync();\n        cur++;", "        asm volatile(\"s_waitcnt lgkmcnt(0)\" ::: \"memory\");\n        cur++;")],
+}
+
+
+def build_variant(name):
+    src_dir = os.path.join(REPO, "xlib", name, "csrc")
+    if os.path.exists(src_dir):
+        shutil.rmtree(src_dir)
+    shutil.copytree(B.CSRC, src_dir, ignore=shutil.ignore_patterns("build*"))
+    p = os.path.join(src_dir, SRC)
+    s = open(p).read()
+    for old, new in VARIANTS[name]:
+        n = s.count(old)
+        if n == 0:
+            raise SystemExit("%s: patch not found: %r" % (name, old[:60]))
+        s = s.replace(old, new)
+    open(p, "w").write(s)
+    objs = []
+    for f in B.SOURCES:
+        obj = os.path.join(src_dir, os.path.splitext(f)[0] + ".o")
+        cmd = [B.HIPCC] + B.FLAGS[:-2] + ["-I", src_dir] + B.PER_FILE.get(f, []) + ["-c", os.path.join(src_dir, f),
+                                                                                  "-o", obj]
+        subprocess.run(cmd, check=True, capture_output=True)
+        objs.append(obj)
+    out = os.path.join(REPO, "xlib", name, "libmli_hip.so")
+    subprocess.run([B.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + objs, check=True)
+    for o in objs:
+        os.remove(o)
+    print("built", out)
+
+
+def run_variant(name, extra):
+    env = dict(os.environ, MLI_HIP_LIB=os.path.join(REPO, "xlib", name, "libmli_hip.so"))
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "30", "--warmup", "3", "--no-cpu",
+           "--pipeline", "off"] + extra
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        print(name, "FAILED", r.stderr[-2000:])
+        return None
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    k = d["kernels"].get("mli_heads_bwd", {})
+    print(json.dumps({"variant": name, "extra": " ".join(extra), "ms_step": d["ms_per_step"],
+                      "heads_bwd_ms": round(k.get("ms_per_launch", 0), 4)}), flush=True)
+    return d
+
+
+if __name__ == "__main__":
+    what = sys.argv[1]
+    names = [a for a in sys.argv[2:] if not a.startswith("--")] or list(VARIANTS)
+    extra = [a for a in sys.argv[2:] if a.startswith("--")]
+    extra = [x for e in extra for x in e.split("=", 1)]
+    for n in names:
+        if what == "build":
+            build_variant(n)
+        else:
+            run_variant(n, extra)
