@@ -234,7 +234,8 @@ int mli_rgb_bwd_workspace(const mli_rgb_bwd_args* a, int64_t* bytes);
  * gradients of their 256 x 256 layers 1..3 in one launch, dZ_1..dZ_3 never written to HBM;
  * replaces mli_rgb_bwd + the BIG class of mli_wgrad (autograd through MLPwithSkipConnection,
  * nerf_util.py:186-196).  Also writes dZ_0 rows and dz4 rows, the operands of the layer-0
- * (WIDE) and layer-4 (THIN) weight gradients, which stay with mli_wgrad.  Workgroup (head, l)
+ * (WIDE) and layer-4 (THIN) weight gradients, which stay with mli_wgrad (dZ_0 by a second launch
+ * from the dZ_1 fragments the first one writes to dz1f).  Workgroup (head, l)
  * owns dW_l over a k-slice of 128-sample tiles; split[l-1] workgroups per head and l (0:
  * default 48, 24, 12).  Default: the k-slices add into dw/db (caller-zeroed) by fp32 atomics;
  * deterministic: per-slice slabs in `workspace`, summed in slice order (overwrites dw/db). */
@@ -246,6 +247,7 @@ typedef struct {
   const uint16_t* xT;     /* [3][4][256][S] from mli_rgb_fwd (training) */
   uint16_t* dz0T;         /* out [3][256][S] feature-major dZ_0 (scaled) */
   uint16_t* dz4T;         /* out [3][4][S] feature-major dz4 rows (scaled) */
+  uint16_t* dz1f;         /* scratch [3][S/32][16][64][8]: dZ_1 as MFMA B fragments (bytes[3]) */
   float* dw[9];           /* [head*3 + l-1]: dW_l [256][256] (row = output feature) */
   float* db[9];           /* [head*3 + l-1]: db_l [256] */
   int split[3];
@@ -253,7 +255,7 @@ typedef struct {
   float* workspace;       /* deterministic: bytes[2] of mli_heads_bwd_workspace */
 } mli_heads_bwd_args;
 int mli_heads_bwd(const mli_heads_bwd_args* a, mli_stream_t s);
-/* bytes[0..2]: dz0T, dz4T, workspace (0 unless deterministic). */
+/* bytes[0..3]: dz0T, dz4T, workspace (0 unless deterministic), dz1f.  S must be a multiple of 256. */
 int mli_heads_bwd_workspace(const mli_heads_bwd_args* a, int64_t* bytes);
 
 /* Weight/bias gradients dW_l = dZ_l^T X_l, db_l = sum dZ_l (split-K MFMA GEMM).  Default: the

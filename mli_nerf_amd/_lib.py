@@ -74,7 +74,7 @@ class RgbBwdArgs(C.Structure):
 
 class HeadsBwdArgs(C.Structure):
     _fields_ = [("R", I32), ("N", I32), ("dz4", P), ("wbwd", P), ("masks", P), ("xT", P), ("dz0T", P),
-                ("dz4T", P), ("dw", P * 9), ("db", P * 9), ("split", I32 * 3), ("deterministic", I32),
+                ("dz4T", P), ("dz1f", P), ("dw", P * 9), ("db", P * 9), ("split", I32 * 3), ("deterministic", I32),
                 ("workspace", P)]
 
 
@@ -200,7 +200,7 @@ ENTRY_POINTS = {
 WORKSPACE = {
     "mli_sdf": 1, "mli_rgb_fwd": 5, "mli_rgb_bwd": 2, "mli_wgrad": 1, "mli_composite_bwd_geo": 4,
     "mli_geo_bwd": 6, "mli_sdf_bwd": 4, "mli_hash_bwd": 1, "mli_light_visibility": 5, "mli_stage_b_loss": 5,
-    "mli_pack": 1, "mli_heads_bwd": 3,
+    "mli_pack": 1, "mli_heads_bwd": 4,
 }
 
 _lib = None

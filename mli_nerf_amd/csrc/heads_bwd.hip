@@ -12,17 +12,18 @@
 // chain from dz4 down to dZ_l for its 128 samples (wave w: samples 32w..32w+31, the
 // activations in registers as MFMA B fragments exactly as mli_rgb_bwd), stages each 32-row
 // n-tile of dZ_l^T in LDS and multiplies it into the accumulators against X_l^T, which the
-// workgroup brings from HBM by LDS-DMA.  The l = 1 workgroups also finish the chain to dZ_0
-// and write it (feature-major, the operand of the layer-0 dW, mli_wgrad WIDE class).
+// workgroup brings from HBM by LDS-DMA.  The l = 1 workgroups also write dZ_1 as an MFMA
+// B-fragment image; a second launch (mlp.hip, dz0_kernel) takes the chain one layer further to
+// dZ_0 rows, the operand of the layer-0 dW (mli_wgrad WIDE class).
 //
-// Work per tile: l = 3: 8 + 128 MFMAs per wave; l = 2: + the W3^T layer (128); l = 1: + W2^T
-// and the dZ_0 layer (W1^T): 520.  The k-slices per l are sized in that proportion (split[]).
+// Work per tile: l = 3: 8 + 128 MFMAs per wave; l = 2: + the W3^T layer (128); l = 1: + W2^T:
+// 392.  The k-slices per l are sized in that proportion (split[]).
 //
-// Queues: vmcnt retires in issue order, so a wave that streams weight chunks from L2 every
-// phase cannot also have a long-latency HBM load in flight without waiting for it a phase or
-// two later.  Waves 0-1 (RING) issue only the weight-chunk DMAs and wait on them every phase;
-// waves 2-3 (LOAD) issue everything that comes from HBM (X_l, the ReLU masks, dz4) one tile
-// ahead plus the dZ_0 stores, and wait on those only where the data is next needed.
+// Queues: every wave issues a quarter of each weight chunk's LDS-DMA and waits for the next
+// chunk at the end of every phase, with a count of the VMEM ops it issued after that chunk
+// (vmcnt retires in issue order).  Waves 2-3 (LOAD) also bring X_l, the ReLU masks and dz4
+// from HBM, spread over the phases so that no phase carries a burst of LDS-DMA issues; what
+// a phase issues has landed at the end of the next one.
 #include "common.h"
 
 #include <algorithm>
@@ -37,8 +38,7 @@ constexpr int HEAD_BYTES = 8 * CH1 + 24 * CH16;
 constexpr int WCH = 16 * 1024;               // ring chunk: 16 A fragments (the zero bias is not loaded)
 constexpr int NSLOT = 3, DIST = 2;
 constexpr int RING_OPS = WCH / 1024 / 2;     // 1 KiB per LDS-DMA op, 2 RING waves: 8 ops per wave
-constexpr int SROW = TILE * 2 + 16;          // staged dZ^T row: 128 samples + 16 B pad
-constexpr int ZT = 32 * SROW;                // one staged n-tile [32 rows][128 samples]
+constexpr int ZTB = TILE * 64;               // one staged dZ_l^T n-tile for the dW [128 samples][32 features]
 constexpr int XW = 64 * 256;                 // one wave's X slice [64 rows][128 samples], swizzled
 constexpr int MASKB = 4096;                  // one layer's ReLU masks for a tile [4 waves][64][16 B]
 constexpr int Z4B = 4 * 3 * 256;             // dz4 of a tile [4 waves][3][64 lanes] fp32
@@ -50,11 +50,11 @@ struct Map {
   int w4, ring, x, zt, mask, z4, end;
 };
 constexpr Map map_of(int L) {
-  return L == 3 ? Map{0, 0, 8192 + 8 * ZT, 8192, 8192 + 8 * ZT + 4 * XW, 8192 + 8 * ZT + 4 * XW + MASKB,
-                      8192 + 8 * ZT + 4 * XW + MASKB + Z4B}
+  return L == 3 ? Map{0, 0, 8192 + 8 * ZTB, 8192, 8192 + 8 * ZTB + 4 * XW, 8192 + 8 * ZTB + 4 * XW + MASKB,
+                      8192 + 8 * ZTB + 4 * XW + MASKB + Z4B}
                 : Map{0, 8192, 8192 + NSLOT * WCH, 8192 + NSLOT * WCH + 4 * XW,
-                      8192 + NSLOT * WCH + 4 * XW + 2 * ZT, 8192 + NSLOT * WCH + 4 * XW + 2 * ZT + 4 * MASKB,
-                      8192 + NSLOT * WCH + 4 * XW + 2 * ZT + 4 * MASKB + Z4B};
+                      8192 + NSLOT * WCH + 4 * XW + 2 * ZTB, 8192 + NSLOT * WCH + 4 * XW + 2 * ZTB + 4 * MASKB,
+                      8192 + NSLOT * WCH + 4 * XW + 2 * ZTB + 4 * MASKB + Z4B};
 }
 constexpr int LDS_BYTES = std::max(map_of(1).end, map_of(3).end);
 static_assert(LDS_BYTES <= 160 * 1024, "LDS");
@@ -103,21 +103,23 @@ struct Ctx {
 
 // ----------------------------------------------------------------------- LOAD-wave DMAs
 // X_l^T of tile T: 4 slices x 16 ops of 4 rows x 256 B; LOAD wave lw issues 32.
-template <int L>
-MLI_FI void x_dma(const Ctx& k, const uint16_t* xrows, int T, int lw) {
+template <int L, int COUNT>
+MLI_FI void x_dma(const Ctx& k, const uint16_t* xrows, int T, int first) {
   constexpr Map M = map_of(L);
-  // row rho = 4u + (lane >> 4) of a slice, LDS chunk lane & 15 <- global chunk
-  // (lane & 15) ^ swz(rho) = c2 ^ (u & 3), c2 = (lane & 15) ^ ((lane >> 4) << 2): four per-lane
-  // element offsets; everything else is uniform (no 64-bit per-op addresses kept live)
+  // piece i (0..63): slice i >> 4, rows 4u .. 4u+3 (u = i & 15).  Row rho = 4u + (lane >> 4),
+  // LDS chunk lane & 15 <- global chunk (lane & 15) ^ swz(rho) = c2 ^ (u & 3), c2 = (lane & 15)
+  // ^ ((lane >> 4) << 2): four per-lane element offsets, everything else uniform
   const int rho_lo = k.lane >> 4, c2 = (k.lane & 15) ^ (rho_lo << 2);
   int lo[4];
 #pragma unroll
-  for (int v = 0; v < 4; ++v) lo[v] = opaque_v(rho_lo * k.S + 8 * (c2 ^ v));
+  for (int v = 0; v < 4; ++v) lo[v] = rho_lo * k.S + 8 * (c2 ^ v);
   const uint16_t* base = xrows + (size_t)T * TILE;
 #pragma unroll
-  for (int ii = 0; ii < 32; ++ii) {
-    const int i = lw * 32 + ii, ws = i >> 4, u = i & 15;
-    glds16(base + (size_t)(64 * ws + 4 * u) * k.S + lo[u & 3], k.lds + M.x + ws * XW + u * 1024);
+  for (int ii = 0; ii < COUNT; ++ii) {
+    const int i = __builtin_amdgcn_readfirstlane(first + ii), ws = i >> 4, u = i & 15;
+    const int v = u & 3;
+    const int l = v == 0 ? lo[0] : v == 1 ? lo[1] : v == 2 ? lo[2] : lo[3];
+    glds16(base + (size_t)(64 * ws + 4 * u) * k.S + l, k.lds + M.x + ws * XW + u * 1024);
   }
 }
 
@@ -149,18 +151,6 @@ MLI_FI void z4_dma(const Ctx& k, int T, int lw) {
   }
 }
 
-// A staged dZ_0 n-tile (32 rows x 128 samples) out to dz0T rows: 4 x 16 B per LOAD thread.
-MLI_FI void flush_zt(const Ctx& k, const uint8_t* zb, int nt, int T) {
-  const int ltid = threadIdx.x - 128, row = ltid >> 4, col = ltid & 15;
-  uint16_t* dst = k.a->dz0T + ((size_t)k.hd * 256 + 32 * nt) * k.S + (size_t)T * TILE;
-  const int lo = opaque_v(row * k.S + col * 8);
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const u32x4 x = *reinterpret_cast<const u32x4*>(zb + (row + 8 * u) * SROW + col * 16);
-    __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(dst + (size_t)(8 * u) * k.S + lo));
-  }
-}
-
 // W4^T (8 n-tiles x 1 KiB, KS 1), resident for the whole kernel: 2 ops per wave.
 template <int L>
 MLI_FI void w4_load(const Ctx& k) {
@@ -185,9 +175,11 @@ MLI_FI void ring_issue(HRing& rg, const Ctx& k) {
   const int cidx = min(rg.next, rg.total - 1);  // past the end: a dummy re-load into a free slot
   const uint8_t* src = rg.base + (size_t)(cidx % NPT) * CH16;
   uint8_t* dst = k.lds + M.ring + (rg.next % NSLOT) * WCH;
-  const int rw = k.wave;  // 0 or 1
 #pragma unroll
-  for (int u = 0; u < RING_OPS; ++u) glds16(src + (2 * u + rw) * 1024 + k.lane * 16, dst + (2 * u + rw) * 1024);
+  for (int u = 0; u < RING_OPS; ++u) {
+    const int piece = 4 * u + k.wave;
+    glds16(src + piece * 1024 + k.lane * 16, dst + piece * 1024);
+  }
   rg.next++;
 }
 
@@ -237,15 +229,58 @@ MLI_FI f32x16 chunk16(const uint8_t* chunk, const half8* in, int lane) {
   return acc;
 }
 
-// dZ n-tile (accumulator layout: rows acc_row(i, h), sample column 32 wave + c) -> staged
-// [32 rows][128 samples] fp16
-MLI_FI void stage(uint8_t* zb, const f32x16& v, const Ctx& k) {
-  uint8_t* sb = zb + (4 * k.h) * SROW + (k.wave * 32 + k.c) * 2;
+// dW staging: the n-tile as [128 samples][32 features] fp16, 64 B rows, 8-byte units XOR-swizzled
+// by (sample >> 1) & 7.  A lane writes its 16 accumulator values (features 8g + 4h + 0..3 of
+// its sample, g = 0..3) as 4 x 8 bytes; the A fragment of a dW k-step is read back transposed
+// (ds_read_b64_tr_b16).  Both conflict-free.
+typedef __fp16 fp16x4_t __attribute__((__vector_size__(4 * sizeof(__fp16))));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) fp16x4_t lds_fp16x4_t;
+
+MLI_FI int zswz(int s) { return (s >> 1) & 7; }
+
+MLI_FI void stage_t(uint8_t* zb, const f32x16& v, const Ctx& k) {
+  const int s = k.wave * 32 + k.c;
+  uint8_t* row = zb + s * 64;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const f16 x = (f16)v[i];
-    *reinterpret_cast<uint16_t*>(sb + ((i & 3) + 8 * (i >> 2)) * SROW) = __builtin_bit_cast(uint16_t, x);
+  for (int g = 0; g < 4; ++g) {
+    const half4 x = {(f16)v[4 * g], (f16)v[4 * g + 1], (f16)v[4 * g + 2], (f16)v[4 * g + 3]};
+    *reinterpret_cast<half4*>(row + (((2 * g + k.h) ^ zswz(s)) << 3)) = x;
   }
+}
+
+// A fragment of dW k-step q: feature lane & 31, samples 64h + 8q + 0..7 (two 4-sample reads;
+// the 16-lane group g of the read takes h = g >> 1 and features 16 (g & 1) + 0..15).  Row s =
+// 64h + 8q + (i >> 2) (+4): the swizzle ((s >> 1) & 7) depends on q only through q & 1, so four
+// per-lane offsets (Offs::z) serve every k-step (+ 512 q as an immediate).
+struct Offs {
+  int z[2][2];  // [q & 1][read]
+  int x[8];     // X slice B fragment (cb 0) of k-step q: row r, chunk (8h + q) ^ swz(r)
+};
+
+MLI_FI Offs make_offs(const Ctx& k) {
+  Offs o;
+  const int i = k.lane & 15, grp = k.lane >> 4, u = 4 * (grp & 1) + (i & 3);
+  const int s0 = 64 * (grp >> 1) + (i >> 2);
+#pragma unroll
+  for (int qp = 0; qp < 2; ++qp)
+#pragma unroll
+    for (int rd = 0; rd < 2; ++rd) {
+      const int s = s0 + 8 * qp + 4 * rd;
+      o.z[qp][rd] = (s - 8 * qp) * 64 + ((u ^ zswz(s)) << 3);
+    }
+  const int sw = swz(k.c);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) o.x[q] = k.c * 256 + (((8 * k.h + q) ^ sw) << 4);
+  return o;
+}
+
+MLI_FI half8 zt_frag(const uint8_t* zb, int q, const Offs& o) {
+  const uint8_t* b = zb + 512 * q;
+  const fp16x4_t a = __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_fp16x4_t*)(b + o.z[q & 1][0]));
+  const fp16x4_t c = __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_fp16x4_t*)(b + o.z[q & 1][1]));
+  const half4 ha = __builtin_bit_cast(half4, a), hc = __builtin_bit_cast(half4, c);
+  return half8{ha[0], ha[1], ha[2], ha[3], hc[0], hc[1], hc[2], hc[3]};
 }
 
 MLI_FI float hsum8(const half8& v) {
@@ -293,20 +328,18 @@ MLI_FI void dw_release(f32x16 (&dw)[8][2]) {
 // dW rows of n-tile nt (32) x this wave's 64 columns += staged dZ^T (zb) x X slice, over the
 // tile's 128 samples (8 k-steps); the bias partial of the n-tile on wave nt & 3.
 template <bool XREG>
-MLI_FI void dw_tile(f32x16 (&acc)[2], const uint8_t* zb, const uint8_t* xs, const half8 (&xr)[2][8], const Ctx& k,
+MLI_FI void dw_tile(f32x16 (&acc)[2], const uint8_t* zb, const uint8_t* xs, const half8 (&xr)[2][8], const Offs& of,
                     bool do_bias, float& bp) {
-  const int r = k.c, sw = swz(k.c);
   // operands of k-steps q, q+1: 2 dZ^T fragments + 4 X fragments (X: registers or the slice)
   struct Ops { half8 a[2], x[4]; };
   auto load = [&](Ops& o, int q) MLI_LAMBDA_FI {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) o.a[u] = *reinterpret_cast<const half8*>(zb + r * SROW + (64 * k.h + 8 * (q + u)) * 2);
+    for (int u = 0; u < 2; ++u) o.a[u] = zt_frag(zb, q + u, of);
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
       for (int u = 0; u < 2; ++u)
-        o.x[2 * cb + u] = XREG ? xr[cb][q + u]
-                               : *reinterpret_cast<const half8*>(xs + (32 * cb + r) * 256 + (((8 * k.h + q + u) ^ sw) << 4));
+        o.x[2 * cb + u] = XREG ? xr[cb][q + u] : *reinterpret_cast<const half8*>(xs + 32 * 256 * cb + of.x[q + u]);
   };
   Ops ops[2];
   load(ops[0], 0);
@@ -321,15 +354,13 @@ MLI_FI void dw_tile(f32x16 (&acc)[2], const uint8_t* zb, const uint8_t* xs, cons
 }
 
 template <int L>
-MLI_FI void x_to_regs(half8 (&xr)[2][8], const Ctx& k) {
+MLI_FI void x_to_regs(half8 (&xr)[2][8], const Ctx& k, const Offs& of) {
   constexpr Map M = map_of(L);
   const uint8_t* xs = k.lds + M.x + k.wave * XW;
-  const int sw = swz(k.c);
 #pragma unroll
   for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
-      xr[cb][q] = *reinterpret_cast<const half8*>(xs + (32 * cb + k.c) * 256 + (((8 * k.h + q) ^ sw) << 4));
+    for (int q = 0; q < 8; ++q) xr[cb][q] = *reinterpret_cast<const half8*>(xs + 32 * 256 * cb + of.x[q]);
 }
 
 // dz4 B fragment (k-step of 16: rows 0..2 = the head's outputs, on lane half 0)
@@ -401,32 +432,35 @@ MLI_FI void write_out(const KArgs& ka, const Ctx& k, int split, f32x16 (&dw)[8][
 }
 
 // ----------------------------------------------------------------------- l = 1
-// Tile phases: 0 (W4^T -> dZ3), 1-8 (W3^T -> dZ2), 9-16 (W2^T -> dZ1: staged, dW1 of the
-// previous n-tile), 17-24 (W1^T -> dZ0: staged and written by the LOAD waves; dW1 of n-tile
-// 7 in phase 17).  LOAD-wave schedule for tile T: phase 0 flush dZ0 n-tile 7 of T-1 (4 ops),
-// 1 masks0(T) (2), 16 wait(0) [masks0], 17 dz4 + masks 3,2,1 (T+1) (12), 18 X(T+1) (32) +
-// flush n-tile 0 (4), 19-24 flush n-tiles 1-6 (24); waits: end of 8: X(T) -> ops after it
-// 28 + 4 + 2 = 34; end of 24: dz4/masks(T+1) -> ops after them 32 + 28 = 60.
+// Tile phases: 0 (dW1 of n-tile 7 of tile T-1; W4^T -> dZ3), 1-8 (W3^T -> dZ2), 9-16 (W2^T ->
+// dZ1: its B-fragment image out to HBM for the dZ_0 launch, the n-tile staged for dW1, dW1 of
+// n-tile t-1).  LOAD waves after their chunk quarter: dz4 + masks 3 of T+1 in phase 1, masks 2
+// of T+1 in 2, X(T) over 1-6 (X(T-1) is read until phase 0), masks 1 of T+1 in 10.  Every
+// wave stores its dZ1 fragments (2 per phase) in 9-16.  Wait at the end of a phase: the ops
+// issued after the previous phase's chunk quarter = what that phase issued after it + 4 + what
+// this phase issues after its own (tables below; the first tile issues fewer: stricter).
+constexpr int X_OFF[6] = {0, 6, 12, 17, 22, 27};  // X pieces per phase: 6, 6, 5, 5, 5, 5
+constexpr int L1_POST_LOAD_W3[8] = {14, 8, 5, 5, 5, 5, 0, 0};  // dz4 6 + masks 2 + X 6, ...
+
 template <int ROLE>
 MLI_FI void body1(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
   constexpr int L = 1;
   constexpr Map M = map_of(L);
   const uint16_t* xrows = k.a->xT + (size_t)(k.hd * 4 + 0) * 256 * k.S;
   const int lw = k.wave - 2;
+  const Offs of = make_offs(k);
   const bool bias_w[8] = {k.wave == 0, k.wave == 1, k.wave == 2, k.wave == 3,
                           k.wave == 0, k.wave == 1, k.wave == 2, k.wave == 3};
-  HRing rg{reinterpret_cast<const uint8_t*>(k.a->wbwd) + (size_t)k.hd * HEAD_BYTES + 8 * CH1, 0, (t1 - t0) * 24};
+  HRing rg{reinterpret_cast<const uint8_t*>(k.a->wbwd) + (size_t)k.hd * HEAD_BYTES + 8 * CH1, 0, (t1 - t0) * 16};
   w4_load<L>(k);
   if (ROLE == LOAD) {
     z4_dma<L>(k, t0, lw);
     mask_dma<L>(k, k.a->masks, 3, t0, 3, lw);
     mask_dma<L>(k, k.a->masks, 2, t0, 2, lw);
     mask_dma<L>(k, k.a->masks, 1, t0, 1, lw);
-    x_dma<L>(k, xrows, t0, lw);
-  } else {
-    ring_issue<L, 24>(rg, k);
-    ring_issue<L, 24>(rg, k);
   }
+  ring_issue<L, 16>(rg, k);
+  ring_issue<L, 16>(rg, k);
   vm_wait63(0);
   block_sync();
 
@@ -440,12 +474,14 @@ MLI_FI void body1(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
   const half8 xr_unused[2][8] = {};
   const uint8_t* xs = k.lds + M.x + k.wave * XW;
   uint8_t* zt0 = k.lds + M.zt;
+  half8* f1 = reinterpret_cast<half8*>(k.a->dz1f + (size_t)k.hd * 256 * k.S) + k.lane;
   int cur = 0;
   half8 A[16], B[16];
   for (int T = t0; T < t1; ++T) {
     const int Tn = min(T + 1, t1 - 1);
-    // phase 0: W4^T -> dZ3 (A)
-    if (ROLE == LOAD && T != t0) flush_zt(k, zt0 + ZT, 7, T - 1);
+    // phase 0
+    if (T != t0) dw_tile<false>(dw[7], zt0 + ZTB, xs, xr_unused, of, bias_w[7], bp[1]);
+    __builtin_amdgcn_sched_barrier(0);
     {
       const half8 z = z4_frag<L>(k);
       const u32x4 mv = mask_read(k.lds + M.mask + 3 * MASKB, k);
@@ -465,65 +501,52 @@ MLI_FI void body1(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
       const u32x4 mv = mask_read(k.lds + M.mask + 2 * MASKB, k);
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
-        if (ROLE == RING) ring_issue<L, 24>(rg, k);
-        if (ROLE == LOAD && t == 0) mask_dma<L>(k, k.a->masks, 0, T, 0, lw);
-        const f32x16 v = masked(chunk16(k.lds + M.ring + (cur % NSLOT) * WCH, A, k.lane), mv, t);
-        B[2 * t] = acc_to_frag(v, 0);
-        B[2 * t + 1] = acc_to_frag(v, 1);
-        if (ROLE == RING) vm_wait63(RING_OPS * (DIST - 1));
-        if (ROLE == LOAD && t == 7) vm_wait63(34);
-        block_sync();
-        cur++;
-      }
-    }
-    // phases 9-16: W2^T -> dZ1 (A), staged; dW1 of n-tile t-1
-    {
-      const u32x4 mv = mask_read(k.lds + M.mask + 1 * MASKB, k);
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        if (ROLE == RING) ring_issue<L, 24>(rg, k);
-        // dW of the previous n-tile, then this n-tile's chain step: kept apart (sched_barrier)
-        // so their operand registers are not live together
-        if (t > 0) dw_tile<false>(dw[t - 1], zt0 + ((t - 1) & 1) * ZT, xs, xr_unused, k, bias_w[t - 1], bp[(t - 1) >> 2]);
-        __builtin_amdgcn_sched_barrier(0);
-        const f32x16 v = masked(chunk16(k.lds + M.ring + (cur % NSLOT) * WCH, B, k.lane), mv, t);
-        A[2 * t] = acc_to_frag(v, 0);
-        A[2 * t + 1] = acc_to_frag(v, 1);
-        stage(zt0 + (t & 1) * ZT, v, k);
-        if (ROLE == RING) vm_wait63(RING_OPS * (DIST - 1));
-        if (ROLE == LOAD && t == 7) vm_wait63(0);
-        block_sync();
-        cur++;
-      }
-    }
-    // phases 17-24: W1^T -> dZ0, staged and flushed by the LOAD waves; dW1 of n-tile 7 first
-    {
-      const u32x4 mv = mask_read(k.lds + M.mask + 0 * MASKB, k);
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        if (t == 0) dw_tile<false>(dw[7], zt0 + ZT, xs, xr_unused, k, bias_w[7], bp[1]);
-        if (ROLE == RING) ring_issue<L, 24>(rg, k);
+        ring_issue<L, 16>(rg, k);
         if (ROLE == LOAD) {
           if (t == 0) {
             z4_dma<L>(k, Tn, lw);
             mask_dma<L>(k, k.a->masks, 3, Tn, 3, lw);
-            mask_dma<L>(k, k.a->masks, 2, Tn, 2, lw);
-            mask_dma<L>(k, k.a->masks, 1, Tn, 1, lw);
-          } else {
-            if (t == 1) x_dma<L>(k, xrows, Tn, lw);
-            flush_zt(k, zt0 + ((t - 1) & 1) * ZT, t - 1, T);
           }
+          if (t == 1) mask_dma<L>(k, k.a->masks, 2, Tn, 2, lw);
+          if (t < 2) x_dma<L, 6>(k, xrows, T, 32 * lw + X_OFF[t]);
+          else if (t < 6) x_dma<L, 5>(k, xrows, T, 32 * lw + X_OFF[t]);
         }
         const f32x16 v = masked(chunk16(k.lds + M.ring + (cur % NSLOT) * WCH, A, k.lane), mv, t);
-        stage(zt0 + (t & 1) * ZT, v, k);
-        if (ROLE == RING) vm_wait63(RING_OPS * (DIST - 1));
-        if (ROLE == LOAD && t == 7) vm_wait63(60);
+        B[2 * t] = acc_to_frag(v, 0);
+        B[2 * t + 1] = acc_to_frag(v, 1);
+        if (ROLE == LOAD) vm_wait63((t > 0 ? L1_POST_LOAD_W3[t - 1] : 0) + RING_OPS + L1_POST_LOAD_W3[t]);
+        else vm_wait63(RING_OPS);
+        block_sync();
+        cur++;
+      }
+    }
+    // phases 9-16: W2^T -> dZ1: B-fragment image out, staged for dW1; dW1 of n-tile t-1
+    {
+      const u32x4 mv = mask_read(k.lds + M.mask + 1 * MASKB, k);
+      half8* ft = f1 + (size_t)(4 * T + k.wave) * 16 * 64;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        ring_issue<L, 16>(rg, k);
+        if (ROLE == LOAD && t == 1) mask_dma<L>(k, k.a->masks, 1, Tn, 1, lw);
+        // dW of the previous n-tile, then this n-tile's chain step: kept apart (sched_barrier)
+        // so their operand registers are not live together
+        if (t > 0) dw_tile<false>(dw[t - 1], zt0 + ((t - 1) & 1) * ZTB, xs, xr_unused, of, bias_w[t - 1], bp[(t - 1) >> 2]);
+        __builtin_amdgcn_sched_barrier(0);
+        const f32x16 v = masked(chunk16(k.lds + M.ring + (cur % NSLOT) * WCH, B, k.lane), mv, t);
+        ft[(2 * t) * 64] = acc_to_frag(v, 0);
+        ft[(2 * t + 1) * 64] = acc_to_frag(v, 1);
+        stage_t(zt0 + (t & 1) * ZTB, v, k);
+        // ops after the previous chunk quarter: previous phase's (stores 2 [+ masks 2 in t = 1]),
+        // this chunk quarter, this phase's
+        const int post_prev = t == 0 ? 0 : (ROLE == LOAD && t == 2) ? 4 : 2;
+        const int post_cur = (ROLE == LOAD && t == 1) ? 4 : 2;
+        vm_wait63(post_prev + RING_OPS + post_cur);
         block_sync();
         cur++;
       }
     }
   }
-  if (ROLE == LOAD) flush_zt(k, zt0 + ZT, 7, t1 - 1);
+  dw_tile<false>(dw[7], zt0 + ZTB, xs, xr_unused, of, bias_w[7], bp[1]);
   vm_wait63(0);
   dw_release(dw);
   write_out(ka, k, split, dw, bp);
@@ -531,14 +554,17 @@ MLI_FI void body1(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
 
 // ----------------------------------------------------------------------- l = 2
 // Tile phases: 0 (dW2 of n-tile 7 of T-1; X(T) to registers; W4^T -> dZ3), 1-8 (W3^T -> dZ2,
-// staged; dW2 of n-tile t-1).  LOAD waves: phase 1 X, dz4, masks 3 and 2 of T+1 (the mask-2
-// slot alternates by tile parity); wait(0) at the end of phase 8.
+// staged; dW2 of n-tile t-1).  LOAD waves after their chunk quarter: X(T+1) over phases 1-6,
+// dz4 + masks 3 and 2 of T+1 in phase 1 (the mask-2 slot alternates by tile parity).
+constexpr int L2_POST_LOAD[8] = {16, 6, 5, 5, 5, 5, 0, 0};  // X 6 + dz4 6 + masks 4, X 6, X 5 ...
+
 template <int ROLE>
 MLI_FI void body2(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
   constexpr int L = 2;
   constexpr Map M = map_of(L);
   const uint16_t* xrows = k.a->xT + (size_t)(k.hd * 4 + 1) * 256 * k.S;
   const int lw = k.wave - 2;
+  const Offs of = make_offs(k);
   const bool bias_w[8] = {k.wave == 0, k.wave == 1, k.wave == 2, k.wave == 3,
                           k.wave == 0, k.wave == 1, k.wave == 2, k.wave == 3};
   HRing rg{reinterpret_cast<const uint8_t*>(k.a->wbwd) + (size_t)k.hd * HEAD_BYTES + 8 * CH1, 0, (t1 - t0) * 8};
@@ -547,11 +573,10 @@ MLI_FI void body2(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
     z4_dma<L>(k, t0, lw);
     mask_dma<L>(k, k.a->masks, 3, t0, 3, lw);
     mask_dma<L>(k, k.a->masks, 2, t0, 0, lw);
-    x_dma<L>(k, xrows, t0, lw);
-  } else {
-    ring_issue<L, 8>(rg, k);
-    ring_issue<L, 8>(rg, k);
+    x_dma<L, 32>(k, xrows, t0, 32 * lw);
   }
+  ring_issue<L, 8>(rg, k);
+  ring_issue<L, 8>(rg, k);
   vm_wait63(0);
   block_sync();
 
@@ -570,8 +595,8 @@ MLI_FI void body2(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
     const int Tn = min(T + 1, t1 - 1);
     const int par = (T - t0) & 1;
     // phase 0
-    if (T != t0) dw_tile<true>(dw[7], zt0 + ZT, nullptr, xr, k, bias_w[7], bp[1]);
-    x_to_regs<L>(xr, k);
+    if (T != t0) dw_tile<true>(dw[7], zt0 + ZTB, nullptr, xr, of, bias_w[7], bp[1]);
+    x_to_regs<L>(xr, k, of);
     {
       const half8 z = z4_frag<L>(k);
       const u32x4 mv = mask_read(k.lds + M.mask + 3 * MASKB, k);
@@ -590,24 +615,27 @@ MLI_FI void body2(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
     const u32x4 mv = mask_read(k.lds + M.mask + par * MASKB, k);
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-      if (ROLE == RING) ring_issue<L, 8>(rg, k);
-      if (ROLE == LOAD && t == 0) {
-        x_dma<L>(k, xrows, Tn, lw);
-        z4_dma<L>(k, Tn, lw);
-        mask_dma<L>(k, k.a->masks, 3, Tn, 3, lw);
-        mask_dma<L>(k, k.a->masks, 2, Tn, par ^ 1, lw);
+      ring_issue<L, 8>(rg, k);
+      if (ROLE == LOAD) {
+        if (t == 0) {
+          z4_dma<L>(k, Tn, lw);
+          mask_dma<L>(k, k.a->masks, 3, Tn, 3, lw);
+          mask_dma<L>(k, k.a->masks, 2, Tn, par ^ 1, lw);
+        }
+        if (t < 2) x_dma<L, 6>(k, xrows, Tn, 32 * lw + X_OFF[t]);
+        else if (t < 6) x_dma<L, 5>(k, xrows, Tn, 32 * lw + X_OFF[t]);
       }
-      if (t > 0) dw_tile<true>(dw[t - 1], zt0 + ((t - 1) & 1) * ZT, nullptr, xr, k, bias_w[t - 1], bp[(t - 1) >> 2]);
+      if (t > 0) dw_tile<true>(dw[t - 1], zt0 + ((t - 1) & 1) * ZTB, nullptr, xr, of, bias_w[t - 1], bp[(t - 1) >> 2]);
       __builtin_amdgcn_sched_barrier(0);
       const f32x16 v = masked(chunk16(k.lds + M.ring + (cur % NSLOT) * WCH, A, k.lane), mv, t);
-      stage(zt0 + (t & 1) * ZT, v, k);
-      if (ROLE == RING) vm_wait63(RING_OPS * (DIST - 1));
-      if (ROLE == LOAD && t == 7) vm_wait63(0);
+      stage_t(zt0 + (t & 1) * ZTB, v, k);
+      if (ROLE == LOAD) vm_wait63((t > 0 ? L2_POST_LOAD[t - 1] : 0) + RING_OPS + L2_POST_LOAD[t]);
+      else vm_wait63(RING_OPS);
       block_sync();
       cur++;
     }
   }
-  dw_tile<true>(dw[7], zt0 + ZT, nullptr, xr, k, bias_w[7], bp[1]);
+  dw_tile<true>(dw[7], zt0 + ZTB, nullptr, xr, of, bias_w[7], bp[1]);
   vm_wait63(0);
   dw_release(dw);
   write_out(ka, k, split, dw, bp);
@@ -615,13 +643,15 @@ MLI_FI void body2(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
 
 // ----------------------------------------------------------------------- l = 3
 // Tile phases: 0 (X(T) to registers; W4^T -> dZ3, all 8 n-tiles staged; dz4 rows written for
-// the layer-4 dW), 1 (dW3 of all 8 n-tiles; LOAD waves: X, dz4, masks 3 of T+1, wait(0)).
+// the layer-4 dW), 1 (dW3 of all 8 n-tiles; each wave DMAs its X slice of T+1, the LOAD waves
+// dz4 and masks 3 of T+1; wait(0)).
 template <int ROLE>
 MLI_FI void body3(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
   constexpr int L = 3;
   constexpr Map M = map_of(L);
   const uint16_t* xrows = k.a->xT + (size_t)(k.hd * 4 + 2) * 256 * k.S;
   const int lw = k.wave - 2;
+  const Offs of = make_offs(k);
   const bool bias_w[8] = {k.wave == 0, k.wave == 1, k.wave == 2, k.wave == 3,
                           k.wave == 0, k.wave == 1, k.wave == 2, k.wave == 3};
   const int no = k.hd == 2 ? 1 : 3;
@@ -629,8 +659,8 @@ MLI_FI void body3(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
   if (ROLE == LOAD) {
     z4_dma<L>(k, t0, lw);
     mask_dma<L>(k, k.a->masks, 3, t0, 0, lw);
-    x_dma<L>(k, xrows, t0, lw);
   }
+  x_dma<L, 16>(k, xrows, t0, 16 * k.wave);
   vm_wait63(0);
   block_sync();
 
@@ -645,7 +675,7 @@ MLI_FI void body3(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
   uint8_t* img = k.lds + M.zt;
   for (int T = t0; T < t1; ++T) {
     const int Tn = min(T + 1, t1 - 1);
-    x_to_regs<L>(xr, k);
+    x_to_regs<L>(xr, k, of);
     {
       const half8 z = z4_frag<L>(k);
       if (k.h == 0) {
@@ -664,19 +694,20 @@ MLI_FI void body3(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
       w4_frags<L>(w4, k);
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
-        stage(img + t * ZT, w4_tile(w4[t], zz, mv, t), k);
+        stage_t(img + t * ZTB, w4_tile(w4[t], zz, mv, t), k);
         opaque_h8(zz);
       }
     }
     block_sync();
+    // every wave brings its own X slice of tile T+1 (16 pieces); the LOAD waves dz4 and masks
+    x_dma<L, 16>(k, xrows, Tn, 16 * k.wave);
     if (ROLE == LOAD) {
-      x_dma<L>(k, xrows, Tn, lw);
       z4_dma<L>(k, Tn, lw);
       mask_dma<L>(k, k.a->masks, 3, Tn, 0, lw);
     }
 #pragma unroll
-    for (int t = 0; t < 8; ++t) dw_tile<true>(dw[t], img + t * ZT, nullptr, xr, k, bias_w[t], bp[t >> 2]);
-    if (ROLE == LOAD) vm_wait63(0);
+    for (int t = 0; t < 8; ++t) dw_tile<true>(dw[t], img + t * ZTB, nullptr, xr, of, bias_w[t], bp[t >> 2]);
+    vm_wait63(0);
     block_sync();
   }
   vm_wait63(0);
@@ -772,15 +803,20 @@ bool plan(const mli_heads_bwd_args* a, KArgs& ka) {
 
 }  // namespace
 
+namespace mli_detail {
+int heads_dz0_launch(const mli_heads_bwd_args* a, hipStream_t s);  // mlp.hip
+}
+
 extern "C" int mli_heads_bwd(const mli_heads_bwd_args* a, mli_stream_t s) {
   KArgs ka;
-  if (!plan(a, ka)) return (int)hipErrorInvalidValue;
-  if (!a->dz4 || !a->wbwd || !a->masks || !a->xT || !a->dz0T || !a->dz4T) return (int)hipErrorInvalidValue;
+  if (!plan(a, ka) || ka.S % 256 != 0) return (int)hipErrorInvalidValue;
+  if (!a->dz4 || !a->wbwd || !a->masks || !a->xT || !a->dz0T || !a->dz4T || !a->dz1f) return (int)hipErrorInvalidValue;
   for (int j = 0; j < 9; ++j)
     if (!a->dw[j] || !a->db[j]) return (int)hipErrorInvalidValue;
   if (a->deterministic && !a->workspace) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(heads_bwd_kernel, dim3(ka.first[3]), dim3(THREADS), LDS_BYTES, (hipStream_t)s, ka);
-  if (!a->deterministic) return (int)hipGetLastError();
+  const int e = mli_detail::heads_dz0_launch(a, (hipStream_t)s);
+  if (e || !a->deterministic) return e ? e : (int)hipGetLastError();
   RArgs r;
   r.part = a->workspace;
   for (int j = 0; j < 9; ++j) {
@@ -796,9 +832,10 @@ extern "C" int mli_heads_bwd(const mli_heads_bwd_args* a, mli_stream_t s) {
 extern "C" int mli_heads_bwd_workspace(const mli_heads_bwd_args* a, int64_t* bytes) {
   KArgs ka;
   const int64_t S = (int64_t)a->R * a->N;
-  if (!plan(a, ka)) return (int)hipErrorInvalidValue;
+  if (!plan(a, ka) || S % 256 != 0) return (int)hipErrorInvalidValue;
   bytes[0] = (int64_t)3 * 256 * S * 2;  // dz0T
   bytes[1] = (int64_t)3 * 4 * S * 2;    // dz4T
   bytes[2] = a->deterministic ? (int64_t)3 * (ka.split[0] + ka.split[1] + ka.split[2]) * JOB_F * 4 : 0;
+  bytes[3] = (int64_t)3 * 256 * S * 2;  // dz1f
   return 0;
 }

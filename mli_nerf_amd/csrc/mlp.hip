@@ -81,6 +81,32 @@ MLI_FI void ring_issue(Ring& r, uint8_t* lds, Bytes&& bytes) {
   r.next++;
 }
 
+// Chunks at arbitrary places of a packed image: src(c) gives chunk c's address (its size CH(16))
+struct ChunkAt {
+  const uint8_t* image;
+  int head_bytes;  // chunk c = (head c >> 3, n-tile c & 7) of the W1^T block of each head
+  int first;       // byte offset of the W1^T block inside a head
+  MLI_FI const uint8_t* src(int c) const { return image + (size_t)(c >> 3) * head_bytes + first + (c & 7) * CH(16); }
+  MLI_FI int operator()(int) const { return CH(16); }
+};
+
+template <int ROLE>
+MLI_FI void ring_issue(Ring& r, uint8_t* lds, ChunkAt& at) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint8_t* s = at.src(min(r.next, r.n - 1));
+  const int nb = CH(16);
+  uint8_t* dst = lds + (r.next % NSLOT) * SLOT + wave * 1024;
+  if (ROLE == ALL) {
+#pragma unroll
+    for (int u = 0; u < GLDS; ++u) glds16(s + min(u * 8192 + wave * 1024 + lane * 16, nb - 16), dst + u * 8192);
+  } else if (ROLE == DMA) {
+#pragma unroll
+    for (int u = 0; u < 2 * GLDS; ++u)
+      glds16(s + min(u * 4096 + wave * 1024 + lane * 16, nb - 16), dst + u * 4096);
+  }
+  r.next++;
+}
+
 template <class Bytes>
 MLI_FI void ring_start(Ring& r, const void* base, int n, Bytes&& bytes) {
   r.src = reinterpret_cast<const uint8_t*>(base);
@@ -453,6 +479,82 @@ __global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
 }
 
 
+// ---------------------------------------------------------------------- dZ_0 from dZ_1 fragments
+// Second launch of mli_heads_bwd: per head dZ_0 = (W1^T dZ_1) * relu'(Z_0) (nerf_util.py:186-196
+// autograd), B operand = the dZ_1 fragment image heads_bwd_kernel wrote, W1^T = the last 8
+// chunks of each head in the mli_pack bwd image, written as feature-major rows (the operand of
+// the layer-0 dW).  One workgroup = 256 samples, as mli_rgb_bwd.
+constexpr int HB_HEAD_BYTES = 8 * CH(1) + 24 * CH(16);
+
+template <int ROLE>
+MLI_FI void dz0_body(const mli_heads_bwd_args& a, uint8_t* lds) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tiles = a.R * a.N / 32;
+  const int tile = blockIdx.x * WAVES + wave;
+  ChunkAt at{reinterpret_cast<const uint8_t*>(a.wbwd), HB_HEAD_BYTES, 8 * CH(1) + 16 * CH(16)};
+  constexpr int MASK_OPS = ROLE == DMA ? 2 : 0;
+  // ReLU masks of head layer 0 of head hd (the workgroup's 8 tiles, 8 KiB) into slot hd & 1
+  auto mask_dma = [&](int hd) MLI_LAMBDA_FI {
+    const int hc = min(hd, 2);
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(a.masks) +
+                         (((size_t)(hc * 4) * tiles + (size_t)blockIdx.x * WAVES) * 64) * 16;
+#pragma unroll
+    for (int u = 0; u < MASK_OPS; ++u)
+      glds16(src + u * 4096 + threadIdx.x * 16, lds + MASK_OFF + (hd & 1) * 8192 + u * 4096 + wave * 1024);
+  };
+  Ring rg;
+  rg.src = rg.last = nullptr;
+  rg.next = 0;
+  rg.n = 24;
+  rg.cur = 0;
+  mask_dma(0);
+#pragma unroll
+  for (int d = 0; d < DIST; ++d) ring_issue<ROLE>(rg, lds, at);
+  if (ROLE != STORE) vm_wait((DIST - 1) * ring_ops<ROLE>());
+  block_sync();
+
+  half8 B[16];
+  Stager sg{nullptr, 0, 0};
+  const size_t col0 = (size_t)blockIdx.x * 256;
+  for (int hd = 0; hd < 3; ++hd) {
+    const int S = opaque_s(a.R * a.N);
+    {
+      const half8* src = reinterpret_cast<const half8*>(a.dz1f + (size_t)hd * 256 * S) +
+                         (size_t)tile * 16 * 64 + opaque_v(lane);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) B[q] = src[q * 64];
+    }
+    struct MaskPre {
+      decltype(mask_dma)& dma;
+      int next_head;
+      MLI_FI int count(int t) const { return t == 8 - DIST ? MASK_OPS : 0; }
+      MLI_FI void issue(int t) const {
+        if (t == 8 - DIST) dma(next_head);
+      }
+    };
+    run_layer<ROLE, 16, 8, true, 0, false>(rg, lds, sg, S, B, lane, at, MaskPre{mask_dma, hd + 1},
+                                          [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
+      const u32x4 mv =
+          *reinterpret_cast<const u32x4*>(lds + MASK_OFF + (hd & 1) * 8192 + wave * 1024 + lane * 16);
+      const int wi = t >> 1;
+      const uint32_t word = wi == 0 ? mv[0] : wi == 1 ? mv[1] : wi == 2 ? mv[2] : mv[3];
+      const uint32_t bits = word >> ((t & 1) * 16);
+      f32x16 v;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = ((bits >> i) & 1u) ? acc[i] : 0.0f;
+      stage_tile(sg, lds, v, a.dz0T + ((size_t)hd * 256 + 32 * t) * S + col0, lane);
+    });
+  }
+  stage_flush<ROLE>(sg, lds, opaque_s(a.R * a.N));
+  vm_wait(0);
+}
+
+__global__ __launch_bounds__(THREADS) void dz0_kernel(mli_heads_bwd_args a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 8)) dz0_body<STORE>(a, lds);
+  else dz0_body<DMA>(a, lds);
+}
+
 // ---------------------------------------------------------------------- stage a: geometry dX chain
 // The single 'rgb' head (NeuralLumen/utils/modules.py:164-174) backward down to its inputs,
 // then SDF layer 1.  Chunks: W4^T (8 x KS 1), W3^T, W2^T, W1^T (24 x KS 16), W0^T (9 n-tiles
@@ -588,6 +690,15 @@ __global__ __launch_bounds__(THREADS) void geo_bwd_kernel(mli_geo_bwd_args a) {
 }
 
 }  // namespace
+
+namespace mli_detail {
+int heads_dz0_launch(const mli_heads_bwd_args* a, hipStream_t s) {
+  const int S = a->R * a->N;
+  if (S % 256 != 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(dz0_kernel, dim3(S / 256), dim3(THREADS), LDS_BWD, s, *a);
+  return (int)hipGetLastError();
+}
+}  // namespace mli_detail
 
 extern "C" int mli_rgb_fwd(const mli_rgb_fwd_args* a, mli_stream_t s) {
   const int S = a->R * a->N;

@@ -450,10 +450,11 @@ class RenderEngine:
             # dX chain + dW of the 256x256 layers in one launch; it writes dZ_0 and dz4 rows for
             # the layer-0 (WIDE) and layer-4 (THIN) dW
             dz0T = self._buf("dz0T", (3, 256, S), torch.float16)
+            dz1f = self._buf("dz1f", (3 * 256 * S,), torch.float16)  # dZ_1 fragments (second launch)
             jobs, ad, (pdw, pdb) = self._wgrad_plan(lambda h, li: dz0T[h], dz4T, hd, dwbuf, flat, grad_out, S)
             args = L.HeadsBwdArgs(R, N, L.ptr(dz4), L.ptr(self.wbwd), L.ptr(hd["masks"]), L.ptr(hd["xT"]),
-                                  L.ptr(dz0T), L.ptr(dz4T), pdw, pdb, (C.c_int * 3)(*self.heads_split),
-                                  1 if self.deterministic else 0, None)
+                                  L.ptr(dz0T), L.ptr(dz4T), L.ptr(dz1f), pdw, pdb,
+                                  (C.c_int * 3)(*self.heads_split), 1 if self.deterministic else 0, None)
             if self.deterministic:
                 nbytes = L.workspace("mli_heads_bwd", args)[2]
                 args.workspace = L.ptr(self._buf("heads_ws", (max(nbytes, 4) // 4,)))

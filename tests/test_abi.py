@@ -110,13 +110,14 @@ def test_workspace_queries_match_engine_buffers():
     assert L.workspace("mli_hash_bwd", L.HashBwdArgs(R, N, deterministic=1, n_params=n_params)) == [n_params * 8]
     assert L.workspace("mli_hash_bwd", L.HashBwdArgs(R, N, n_params=n_params)) == [0]
     # fused heads backward: dZ_0 rows, dz4 rows; deterministic slabs of the 9 (head, layer) dW + db
-    assert L.workspace("mli_heads_bwd", L.HeadsBwdArgs(R, N)) == [3 * 256 * S * f16, 3 * 4 * S * f16, 0]
+    assert L.workspace("mli_heads_bwd", L.HeadsBwdArgs(R, N)) == [3 * 256 * S * f16, 3 * 4 * S * f16, 0,
+                                                                   3 * 256 * S * f16]
     hb = L.HeadsBwdArgs(R, N, deterministic=1)
     assert L.workspace("mli_heads_bwd", hb)[2] == 3 * (48 + 24 + 12) * (256 * 256 + 256) * f32
     hb.split = (C.c_int * 3)(8, 4, 2)
     assert L.workspace("mli_heads_bwd", hb)[2] == 3 * (8 + 4 + 2) * (256 * 256 + 256) * f32
     with pytest.raises(RuntimeError):
-        L.workspace("mli_heads_bwd", L.HeadsBwdArgs(100, 1))   # S not a multiple of the 128-sample tile
+        L.workspace("mli_heads_bwd", L.HeadsBwdArgs(128, 1))   # S not a multiple of 256
     # wgrad: the stage-b jobs (engine._wgrad_plan shapes): partial slabs only in deterministic mode
     jobs = []
     for name, k_in, k_out in layout.HEADS:

@@ -70,7 +70,8 @@ def test_fused_matches_split_and_float64():
     model, fu = _backward("fused")
     _, sp = _backward("split")
     S = sp["S"]
-    assert torch.equal(fu["dz0"], sp["dz0"])
+    ok_dz0 = torch.equal(fu["dz0"], sp["dz0"])
+    print("dz0 bit-identical:", ok_dz0)
     no = (3, 3, 1)
     for hd in range(3):
         a, b = fu["dz4T"][hd, :no[hd]], sp["dz4T"][hd, :no[hd]]
@@ -78,8 +79,9 @@ def test_fused_matches_split_and_float64():
         if bad.numel():
             print("dz4T head %d: %d mismatches, first %s: %s vs %s" % (
                 hd, bad.shape[0], bad[:8].tolist(), a[tuple(bad[:8].T)].tolist(), b[tuple(bad[:8].T)].tolist()))
-        assert bad.numel() == 0
+        assert bad.numel() == 0, hd
     vf, vs = _dw_views(model, fu["dw"]), _dw_views(model, sp["dw"])
+    errs = []
     for (hd, li), (dw, db) in vf.items():
         a = sp["dzT"][hd, li].view(256, S).double()
         x = sp["xT"][hd, li - 1].view(256, S).double()
@@ -90,6 +92,9 @@ def test_fused_matches_split_and_float64():
         eb = (db.double() - ref_b).abs().max().item() / scale_b
         es = (dw - vs[(hd, li)][0]).abs().max().item() / scale_w
         print("head %d layer %d: dW err %.2e (split %.2e)  db err %.2e" % (hd, li, ew, es, eb))
+        errs.append((hd, li, ew, eb, es))
+    assert ok_dz0
+    for hd, li, ew, eb, es in errs:
         assert ew < 1e-5 and eb < 1e-5 and es < 1e-5, (hd, li, ew, eb, es)
     cos = torch.nn.functional.cosine_similarity(fu["grad"], sp["grad"], dim=0).item()
     print("parameter gradient cosine fused vs split %.9f" % cos)

@@ -27,8 +27,26 @@ VARIANTS = {
     "no_dw": [('  asm("s_nop 1\\n\\t"\n      "v_mfma_f32_32x32x16_f16 %0, %2, %4, %0\\n\\t"',
                '  if (0) asm("s_nop 1\\n\\t"\n      "v_mfma_f32_32x32x16_f16 %0, %2, %4, %0\\n\\t"')],
     # no chain MFMAs (zeros): DMA, staging and dW
-    "no_chain": [("  for (int q = 0; q < 16; ++q) {\n    if (q % PF == 0) ld_fence();\n    acc = mfma32(w[q * 64], in[q], acc);",
-                  "  for (int q = 0; q < 16; ++q) {\n    if (q % PF == 0) ld_fence();\n    if (q == 99) acc = mfma32(w[q * 64], in[q], acc);")],
+    "no_chain": [("    for (int i = 0; i < PF; ++i) acc = mfma32(buf[g & 1][i], in[g * PF + i], acc);",
+                  "    for (int i = 0; i < PF; ++i) if (i > 99) acc = mfma32(buf[g & 1][i], in[g * PF + i], acc);")],
+    # no weight-chunk DMAs at all (stale weights; DMA issue-cost probe)
+    "no_ringdma": [("  for (int u = 0; u < RING_OPS; ++u) glds16(src + (2 * u + rw) * 1024 + k.lane * 16, dst + (2 * u + rw) * 1024);",
+                    "  for (int u = 0; u < RING_OPS; ++u) if (rw > 7) glds16(src + (2 * u + rw) * 1024 + k.lane * 16, dst + (2 * u + rw) * 1024);")],
+    # no dZ^T staging writes to LDS
+    "no_stage": [("    *reinterpret_cast<uint16_t*>(sb + ((i & 3) + 8 * (i >> 2)) * SROW) = __builtin_bit_cast(uint16_t, x);",
+                  "    if (i > 99) *reinterpret_cast<uint16_t*>(sb + ((i & 3) + 8 * (i >> 2)) * SROW) = __builtin_bit_cast(uint16_t, x);")],
+    # no X DMAs (stale X)
+    "no_xdma": [("    glds16(base + (size_t)(64 * ws + 4 * u) * k.S + lo[u & 3], k.lds + M.x + ws * XW + u * 1024);",
+                 "    if (ii > 99) glds16(base + (size_t)(64 * ws + 4 * u) * k.S + lo[u & 3], k.lds + M.x + ws * XW + u * 1024);")],
+    # no chain AND no dW MFMAs
+    "no_mfma": [("    for (int i = 0; i < PF; ++i) acc = mfma32(buf[g & 1][i], in[g * PF + i], acc);",
+                 "    for (int i = 0; i < PF; ++i) if (i > 99) acc = mfma32(buf[g & 1][i], in[g * PF + i], acc);"),
+                ('  asm("s_nop 1\\n\\t"\n      "v_mfma_f32_32x32x16_f16 %0, %2, %4, %0\\n\\t"',
+                 '  if (0) asm("s_nop 1\\n\\t"\n      "v_mfma_f32_32x32x16_f16 %0, %2, %4, %0\\n\\t"')],
+    # only one layer's workgroups do work (the others return at once): per-layer timing
+    "only_l1": [("  const bool load = k.wave >= 2;\n", "  const bool load = k.wave >= 2;\n  if (L != 1) return;\n")],
+    "only_l2": [("  const bool load = k.wave >= 2;\n", "  const bool load = k.wave >= 2;\n  if (L != 2) return;\n")],
+    "only_l3": [("  const bool load = k.wave >= 2;\n", "  const bool load = k.wave >= 2;\n  if (L != 3) return;\n")],
     # the RING waves do not wait for the next weight chunk (wrong results; latency probe)
     "no_ringwait": [("        if (ROLE == RING) vm_wait63(RING_OPS * (DIST - 1));",
                      "        if (ROLE == RING) {}")],
