@@ -371,7 +371,7 @@ def main():
                     help="train: prefetch the next batch's geometry (sampling/FIELD) on a side stream, "
                          "gated as Trainer.prefetch_gate (heads: after the heads forward of the step in "
                          "flight); measured 4.77 vs 5.07 ms/step off (profiles/r2/s7)")
-    ap.add_argument("--heads-bwd", choices=("fused", "split"), default="fused",
+    ap.add_argument("--heads-bwd", choices=("fused", "split"), default="split",
                     help="stage-b heads backward: fused (mli_heads_bwd: dX chain + 256x256 dW in one launch) "
                          "or split (mli_rgb_bwd + mli_wgrad BIG)")
     ap.add_argument("--heads-split", default="0,0,0",

@@ -11,7 +11,18 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef __fp16 fp16x4_t __attribute__((__vector_size__(4 * sizeof(__fp16))));
+typedef __attribute__((address_space(3))) fp16x4_t lds_fp16x4_t;
+
 #define MLI_FI __device__ __forceinline__
+
+// ds_read_b64_tr_b16 (gfx950): a 16-lane group reads a 4-row x 16-column block of 16-bit
+// elements; lane 4q+p of the group supplies the address of row q, columns 4p..4p+3 (8 B),
+// lane i receives column i of the 4 rows (row q in element q).  EXEC must be all ones.
+MLI_FI half4 ds_read_tr16(const void* lds_addr) {
+  return __builtin_bit_cast(half4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_fp16x4_t*)lds_addr));
+}
 #define MLI_LAMBDA_FI __attribute__((always_inline))
 
 // D = A(32x16) * B(16x32) + C on one wave (gfx950 v_mfma_f32_32x32x16_f16).

@@ -19,11 +19,11 @@
 // Work per tile: l = 3: 8 + 128 MFMAs per wave; l = 2: + the W3^T layer (128); l = 1: + W2^T:
 // 392.  The k-slices per l are sized in that proportion (split[]).
 //
-// Queues: every wave issues a quarter of each weight chunk's LDS-DMA and waits for the next
-// chunk at the end of every phase, with a count of the VMEM ops it issued after that chunk
-// (vmcnt retires in issue order).  Waves 2-3 (LOAD) also bring X_l, the ReLU masks and dz4
-// from HBM, spread over the phases so that no phase carries a burst of LDS-DMA issues; what
-// a phase issues has landed at the end of the next one.
+// Queues: vmcnt retires in issue order, so a wave that waits for the next weight chunk every
+// phase cannot also have a long-latency HBM load in flight.  Waves 0-1 (RING) issue the weight
+// chunk DMAs and wait for them every phase (counted: their own stores after a chunk may stay
+// in flight); waves 2-3 (LOAD) bring X_l, the ReLU masks and dz4 from HBM well ahead and wait
+// for them only where the data is next needed.
 #include "common.h"
 
 #include <algorithm>
@@ -37,7 +37,7 @@ constexpr int CH16 = 16 * 1024 + 128;        //   W3^T, W2^T, W1^T chunk stride
 constexpr int HEAD_BYTES = 8 * CH1 + 24 * CH16;
 constexpr int WCH = 16 * 1024;               // ring chunk: 16 A fragments (the zero bias is not loaded)
 constexpr int NSLOT = 3, DIST = 2;
-constexpr int RING_OPS = WCH / 1024 / 2;     // 1 KiB per LDS-DMA op, 2 RING waves: 8 ops per wave
+constexpr int RING_OPS = WCH / 1024 / 2;     // 1 KiB per LDS-DMA op, 2 RING waves: 8 ops each
 constexpr int ZTB = TILE * 64;               // one staged dZ_l^T n-tile for the dW [128 samples][32 features]
 constexpr int XW = 64 * 256;                 // one wave's X slice [64 rows][128 samples], swizzled
 constexpr int MASKB = 4096;                  // one layer's ReLU masks for a tile [4 waves][64][16 B]
@@ -177,7 +177,7 @@ MLI_FI void ring_issue(HRing& rg, const Ctx& k) {
   uint8_t* dst = k.lds + M.ring + (rg.next % NSLOT) * WCH;
 #pragma unroll
   for (int u = 0; u < RING_OPS; ++u) {
-    const int piece = 4 * u + k.wave;
+    const int piece = 2 * u + k.wave;  // RING waves 0, 1
     glds16(src + piece * 1024 + k.lane * 16, dst + piece * 1024);
   }
   rg.next++;
@@ -233,9 +233,6 @@ MLI_FI f32x16 chunk16(const uint8_t* chunk, const half8* in, int lane) {
 // by (sample >> 1) & 7.  A lane writes its 16 accumulator values (features 8g + 4h + 0..3 of
 // its sample, g = 0..3) as 4 x 8 bytes; the A fragment of a dW k-step is read back transposed
 // (ds_read_b64_tr_b16).  Both conflict-free.
-typedef __fp16 fp16x4_t __attribute__((__vector_size__(4 * sizeof(__fp16))));
-typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) fp16x4_t lds_fp16x4_t;
 
 MLI_FI int zswz(int s) { return (s >> 1) & 7; }
 
@@ -434,13 +431,11 @@ MLI_FI void write_out(const KArgs& ka, const Ctx& k, int split, f32x16 (&dw)[8][
 // ----------------------------------------------------------------------- l = 1
 // Tile phases: 0 (dW1 of n-tile 7 of tile T-1; W4^T -> dZ3), 1-8 (W3^T -> dZ2), 9-16 (W2^T ->
 // dZ1: its B-fragment image out to HBM for the dZ_0 launch, the n-tile staged for dW1, dW1 of
-// n-tile t-1).  LOAD waves after their chunk quarter: dz4 + masks 3 of T+1 in phase 1, masks 2
-// of T+1 in 2, X(T) over 1-6 (X(T-1) is read until phase 0), masks 1 of T+1 in 10.  Every
-// wave stores its dZ1 fragments (2 per phase) in 9-16.  Wait at the end of a phase: the ops
-// issued after the previous phase's chunk quarter = what that phase issued after it + 4 + what
-// this phase issues after its own (tables below; the first tile issues fewer: stricter).
+// n-tile t-1).  LOAD waves: dz4 + masks 3 of T+1 in phase 1, masks 2 of T+1 in 2, X(T) over 1-6
+// (X(T-1) is read until phase 0), masks 1 of T+1 in 10; wait(0) at the end of 8 and 16.  Every
+// wave stores its dZ1 fragments (2 per phase) in 9-16: the RING waves' wait at the end of a
+// phase allows the ops issued after the previous chunk: 8 (W3^T), 10 (first W2^T), 12 (W2^T).
 constexpr int X_OFF[6] = {0, 6, 12, 17, 22, 27};  // X pieces per phase: 6, 6, 5, 5, 5, 5
-constexpr int L1_POST_LOAD_W3[8] = {14, 8, 5, 5, 5, 5, 0, 0};  // dz4 6 + masks 2 + X 6, ...
 
 template <int ROLE>
 MLI_FI void body1(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
@@ -458,9 +453,10 @@ MLI_FI void body1(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
     mask_dma<L>(k, k.a->masks, 3, t0, 3, lw);
     mask_dma<L>(k, k.a->masks, 2, t0, 2, lw);
     mask_dma<L>(k, k.a->masks, 1, t0, 1, lw);
+  } else {
+    ring_issue<L, 16>(rg, k);
+    ring_issue<L, 16>(rg, k);
   }
-  ring_issue<L, 16>(rg, k);
-  ring_issue<L, 16>(rg, k);
   vm_wait63(0);
   block_sync();
 
@@ -501,7 +497,7 @@ MLI_FI void body1(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
       const u32x4 mv = mask_read(k.lds + M.mask + 2 * MASKB, k);
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
-        ring_issue<L, 16>(rg, k);
+        if (ROLE == RING) ring_issue<L, 16>(rg, k);
         if (ROLE == LOAD) {
           if (t == 0) {
             z4_dma<L>(k, Tn, lw);
@@ -514,8 +510,8 @@ MLI_FI void body1(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
         const f32x16 v = masked(chunk16(k.lds + M.ring + (cur % NSLOT) * WCH, A, k.lane), mv, t);
         B[2 * t] = acc_to_frag(v, 0);
         B[2 * t + 1] = acc_to_frag(v, 1);
-        if (ROLE == LOAD) vm_wait63((t > 0 ? L1_POST_LOAD_W3[t - 1] : 0) + RING_OPS + L1_POST_LOAD_W3[t]);
-        else vm_wait63(RING_OPS);
+        if (ROLE == RING) vm_wait63(RING_OPS);
+        if (ROLE == LOAD && t == 7) vm_wait63(0);
         block_sync();
         cur++;
       }
@@ -526,7 +522,7 @@ MLI_FI void body1(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
       half8* ft = f1 + (size_t)(4 * T + k.wave) * 16 * 64;
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
-        ring_issue<L, 16>(rg, k);
+        if (ROLE == RING) ring_issue<L, 16>(rg, k);
         if (ROLE == LOAD && t == 1) mask_dma<L>(k, k.a->masks, 1, Tn, 1, lw);
         // dW of the previous n-tile, then this n-tile's chain step: kept apart (sched_barrier)
         // so their operand registers are not live together
@@ -536,11 +532,8 @@ MLI_FI void body1(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
         ft[(2 * t) * 64] = acc_to_frag(v, 0);
         ft[(2 * t + 1) * 64] = acc_to_frag(v, 1);
         stage_t(zt0 + (t & 1) * ZTB, v, k);
-        // ops after the previous chunk quarter: previous phase's (stores 2 [+ masks 2 in t = 1]),
-        // this chunk quarter, this phase's
-        const int post_prev = t == 0 ? 0 : (ROLE == LOAD && t == 2) ? 4 : 2;
-        const int post_cur = (ROLE == LOAD && t == 1) ? 4 : 2;
-        vm_wait63(post_prev + RING_OPS + post_cur);
+        if (ROLE == RING) vm_wait63(RING_OPS + (t == 0 ? 2 : 4));
+        if (ROLE == LOAD && t == 7) vm_wait63(0);
         block_sync();
         cur++;
       }
@@ -554,9 +547,8 @@ MLI_FI void body1(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
 
 // ----------------------------------------------------------------------- l = 2
 // Tile phases: 0 (dW2 of n-tile 7 of T-1; X(T) to registers; W4^T -> dZ3), 1-8 (W3^T -> dZ2,
-// staged; dW2 of n-tile t-1).  LOAD waves after their chunk quarter: X(T+1) over phases 1-6,
-// dz4 + masks 3 and 2 of T+1 in phase 1 (the mask-2 slot alternates by tile parity).
-constexpr int L2_POST_LOAD[8] = {16, 6, 5, 5, 5, 5, 0, 0};  // X 6 + dz4 6 + masks 4, X 6, X 5 ...
+// staged; dW2 of n-tile t-1).  LOAD waves: X(T+1) over phases 1-6, dz4 + masks 3 and 2 of T+1
+// in phase 1 (the mask-2 slot alternates by tile parity); wait(0) at the end of phase 8.
 
 template <int ROLE>
 MLI_FI void body2(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
@@ -574,9 +566,10 @@ MLI_FI void body2(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
     mask_dma<L>(k, k.a->masks, 3, t0, 3, lw);
     mask_dma<L>(k, k.a->masks, 2, t0, 0, lw);
     x_dma<L, 32>(k, xrows, t0, 32 * lw);
+  } else {
+    ring_issue<L, 8>(rg, k);
+    ring_issue<L, 8>(rg, k);
   }
-  ring_issue<L, 8>(rg, k);
-  ring_issue<L, 8>(rg, k);
   vm_wait63(0);
   block_sync();
 
@@ -615,7 +608,7 @@ MLI_FI void body2(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
     const u32x4 mv = mask_read(k.lds + M.mask + par * MASKB, k);
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-      ring_issue<L, 8>(rg, k);
+      if (ROLE == RING) ring_issue<L, 8>(rg, k);
       if (ROLE == LOAD) {
         if (t == 0) {
           z4_dma<L>(k, Tn, lw);
@@ -629,8 +622,8 @@ MLI_FI void body2(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
       __builtin_amdgcn_sched_barrier(0);
       const f32x16 v = masked(chunk16(k.lds + M.ring + (cur % NSLOT) * WCH, A, k.lane), mv, t);
       stage_t(zt0 + (t & 1) * ZTB, v, k);
-      if (ROLE == LOAD) vm_wait63((t > 0 ? L2_POST_LOAD[t - 1] : 0) + RING_OPS + L2_POST_LOAD[t]);
-      else vm_wait63(RING_OPS);
+      if (ROLE == RING) vm_wait63(RING_OPS);
+      if (ROLE == LOAD && t == 7) vm_wait63(0);
       block_sync();
       cur++;
     }
@@ -643,8 +636,9 @@ MLI_FI void body2(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
 
 // ----------------------------------------------------------------------- l = 3
 // Tile phases: 0 (X(T) to registers; W4^T -> dZ3, all 8 n-tiles staged; dz4 rows written for
-// the layer-4 dW), 1 (dW3 of all 8 n-tiles; each wave DMAs its X slice of T+1, the LOAD waves
-// dz4 and masks 3 of T+1; wait(0)).
+// the layer-4 dW), 1 (dW3 of the 8 n-tiles; every wave DMAs its own X slice of T+1, the LOAD
+// waves dz4 and masks 3 of T+1; wait(0)).  (X_3 loaded straight into registers instead, double
+// buffered, measured slower: 64 rows per load instruction.)
 template <int ROLE>
 MLI_FI void body3(const KArgs& ka, const Ctx& k, int t0, int t1, int split) {
   constexpr int L = 3;

@@ -94,7 +94,7 @@ class RenderEngine:
         # stage-b heads backward: "fused" = mli_heads_bwd (dX chain + the 256x256 dW in one
         # launch, dZ_1..3 stay on chip) + the WIDE/THIN dW; "split" = mli_rgb_bwd + mli_wgrad
         # BIG/WIDE/THIN (dZ_0..3 through HBM)
-        self.heads_bwd = "fused"
+        self.heads_bwd = "split"
         self.heads_split = (0, 0, 0)  # mli_heads_bwd workgroups per (head, layer 1..3); 0 = default
         self._wplans = {}   # wgrad plans per buffer set (the prefetch lanes alternate)
         # reference column -> packed k maps of the head layers (constant; uploaded once)

@@ -253,7 +253,7 @@ class Model(torch.nn.Module):
         self._sdf_version = None
         self.image_width = self.image_size_train[1]
         self.deterministic = False  # fixed-order gradient reductions (RenderEngine.deterministic)
-        self.heads_bwd = "fused"    # stage-b heads backward kernels (RenderEngine.heads_bwd)
+        self.heads_bwd = "split"    # stage-b heads backward kernels (RenderEngine.heads_bwd)
         self.heads_split = (0, 0, 0)
 
     # -------------------------------------------------------------- parameter plumbing

@@ -47,6 +47,31 @@ VARIANTS = {
     "only_l1": [("  const bool load = k.wave >= 2;\n", "  const bool load = k.wave >= 2;\n  if (L != 1) return;\n")],
     "only_l2": [("  const bool load = k.wave >= 2;\n", "  const bool load = k.wave >= 2;\n  if (L != 2) return;\n")],
     "only_l3": [("  const bool load = k.wave >= 2;\n", "  const bool load = k.wave >= 2;\n  if (L != 3) return;\n")],
+    # every wave drains its queue at the end of every phase (counted-wait check)
+    "wait0": [("MLI_FI void vm_wait63(int n) {\n  switch (n) {", "MLI_FI void vm_wait63(int n) {\n  n = 0;\n  switch (n) {")],
+    # weight chunks DMA'd by waves 0-1 only (8 pieces each), every wave drains every phase
+    "ring2_wait0": [("MLI_FI void vm_wait63(int n) {\n  switch (n) {", "MLI_FI void vm_wait63(int n) {\n  n = 0;\n  switch (n) {"),
+                    ("constexpr int RING_OPS = WCH / 1024 / 4; ", "constexpr int RING_OPS = WCH / 1024 / 2; "),
+                    ("    const int piece = 4 * u + k.wave;\n    glds16(", "    const int piece = 2 * u + k.wave;\n    if (k.wave < 2) glds16(")],
+    # mlp.hip stager: no LDS staging writes / no flush (heads forward + rgb_bwd; timing only)
+    "mlp_no_stagew": [("mlp.hip", "    *reinterpret_cast<uint16_t*>(sb + ((i & 3) + 8 * (i >> 2)) * SROW) = __builtin_bit_cast(uint16_t, x);",
+                       "    if (i > 99) *reinterpret_cast<uint16_t*>(sb + ((i & 3) + 8 * (i >> 2)) * SROW) = __builtin_bit_cast(uint16_t, x);")],
+    "mlp_no_flush": [("mlp.hip", "    __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(g + u * step));",
+                      "    if (u > 99) __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(g + u * step));")],
+    # transposed stager: no b64 staging writes / no tr reads in the flush (timing only)
+    "tst_no_w": [("mlp.hip", "    *reinterpret_cast<half4*>(row + (((2 * g + h) ^ sswz(s)) << 3)) = x;",
+                  "    if (g > 99) *reinterpret_cast<half4*>(row + (((2 * g + h) ^ sswz(s)) << 3)) = x;")],
+    "tst_no_r": [("mlp.hip", "    const half4 a = ds_read_tr16(sb + 1024 * NW * u + l0);\n    const half4 b = ds_read_tr16(sb + 1024 * NW * u + l1);",
+                  "    const half4 a = {}; const half4 b = {};")],
+    "tst_no_wr": [("mlp.hip", "    *reinterpret_cast<half4*>(row + (((2 * g + h) ^ sswz(s)) << 3)) = x;",
+                   "    if (g > 99) *reinterpret_cast<half4*>(row + (((2 * g + h) ^ sswz(s)) << 3)) = x;"),
+                  ("mlp.hip", "    const half4 a = ds_read_tr16(sb + 1024 * NW * u + l0);\n    const half4 b = ds_read_tr16(sb + 1024 * NW * u + l1);",
+                   "    const half4 a = {}; const half4 b = {};")],
+    "tst_no_flush": [("mlp.hip", "    __builtin_nontemporal_store(__builtin_bit_cast(u32x4, x),",
+                      "    if (u > 99) __builtin_nontemporal_store(__builtin_bit_cast(u32x4, x),")],
+    # mlp.hip flush: plain (write-back) stores instead of non-temporal
+    "flush_plain": [("mlp.hip", "    __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(g + u * step));",
+                     "    *reinterpret_cast<u32x4*>(g + u * step) = x;")],
     # the RING waves do not wait for the next weight chunk (wrong results; latency probe)
     "no_ringwait": [("        if (ROLE == RING) vm_wait63(RING_OPS * (DIST - 1));",
                      "        if (ROLE == RING) {}")],
@@ -60,14 +85,13 @@ def build_variant(name):
     if os.path.exists(src_dir):
         shutil.rmtree(src_dir)
     shutil.copytree(B.CSRC, src_dir, ignore=shutil.ignore_patterns("build*"))
-    p = os.path.join(src_dir, SRC)
-    s = open(p).read()
-    for old, new in VARIANTS[name]:
-        n = s.count(old)
-        if n == 0:
+    for patch in VARIANTS[name]:
+        fname, old, new = patch if len(patch) == 3 else (SRC,) + tuple(patch)
+        p = os.path.join(src_dir, fname)
+        s = open(p).read()
+        if s.count(old) == 0:
             raise SystemExit("%s: patch not found: %r" % (name, old[:60]))
-        s = s.replace(old, new)
-    open(p, "w").write(s)
+        open(p, "w").write(s.replace(old, new))
     objs = []
     for f in B.SOURCES:
         obj = os.path.join(src_dir, os.path.splitext(f)[0] + ".o")
@@ -91,9 +115,9 @@ def run_variant(name, extra):
         print(name, "FAILED", r.stderr[-2000:])
         return None
     d = json.loads(r.stdout.strip().splitlines()[-1])
-    k = d["kernels"].get("mli_heads_bwd", {})
-    print(json.dumps({"variant": name, "extra": " ".join(extra), "ms_step": d["ms_per_step"],
-                      "heads_bwd_ms": round(k.get("ms_per_launch", 0), 4)}), flush=True)
+    ks = {n: round(v["ms_per_launch"], 4) for n, v in d["kernels"].items()
+          if n in ("mli_heads_bwd", "mli_rgb_fwd", "mli_rgb_bwd", "mli_wgrad:big")}
+    print(json.dumps({"variant": name, "extra": " ".join(extra), "ms_step": d["ms_per_step"], "kernels": ks}), flush=True)
     return d
 
 
