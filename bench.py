@@ -371,6 +371,9 @@ def main():
                     help="train: prefetch the next batch's geometry (sampling/FIELD) on a side stream, "
                          "gated as Trainer.prefetch_gate (heads: after the heads forward of the step in "
                          "flight); measured 4.77 vs 5.07 ms/step off (profiles/r2/s7)")
+    ap.add_argument("--priority", choices=("none", "main", "side"), default="none",
+                    help="pipeline: run the step on a high-priority stream (main) or give the prefetch "
+                         "stream the high priority (side)")
     ap.add_argument("--heads-bwd", choices=("fused", "split"), default="split",
                     help="stage-b heads backward: fused (mli_heads_bwd: dX chain + 256x256 dW in one launch) "
                          "or split (mli_rgb_bwd + mli_wgrad BIG)")
@@ -448,6 +451,14 @@ def main():
     # --pipeline: step k draws batch k+1 and issues its geometry (rays, sampling rounds, FIELD:
     # frozen SDF) on a side stream (Trainer.prefetch), and trains on batch k.  Every timed step
     # still draws, samples, renders and trains one full batch.  On by default (gate heads).
+    # stream priorities (experiment): torch range (lowest, highest)
+    lo, hi = torch.cuda.Stream.priority_range()
+    if args.priority == "side":
+        trainer.side_priority = hi
+    main_stream = torch.cuda.Stream(device=dev, priority=hi) if args.priority == "main" else None
+    if main_stream is not None:
+        torch.cuda.synchronize()
+        torch.cuda.set_stream(main_stream)
     pipe = args.pipeline != "off" and model.stage == "b"
     cur = next_batch()
     if pipe:

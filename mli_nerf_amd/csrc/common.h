@@ -41,12 +41,23 @@ MLI_FI int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 MLI_FI int k_nat(int q, int h, int j) { return 16 * q + 8 * h + j; }
 MLI_FI int k_acc(int q, int h, int j) { return 16 * q + 8 * (j >> 2) + 4 * h + (j & 3); }
 
-// Convert accumulator registers [8s, 8s+8) to the fp16 B fragment of k-step 2t+s.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 half2 __attribute__((ext_vector_type(2)));
+
+// Convert accumulator registers [8s, 8s+8) to the fp16 B fragment of k-step 2t+s: four
+// v_cvt_pk_f16_f32 (round to nearest even, as the element-wise cast).  Written pairwise so the
+// fragment is built from packed words; element-wise casts whose halves are also needed one by
+// one (LDS staging) were assembled from 16 v_cvt_f16_f32 + 64 v_perm_b32 per 32 x 32 tile.
 MLI_FI half8 acc_to_frag(const f32x16& v, int s) {
-  half8 o;
+  u32x4 w;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = (f16)v[8 * s + j];
-  return o;
+  for (int p = 0; p < 4; ++p) {
+    f32x2 f;
+    f.x = v[8 * s + 2 * p];
+    f.y = v[8 * s + 2 * p + 1];
+    w[p] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f, half2));
+  }
+  return __builtin_bit_cast(half8, w);
 }
 
 MLI_FI float softplus100(float x) {
@@ -114,12 +125,19 @@ MLI_FI void glds16(const void* g, uint8_t* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((gbl_cvoid_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
 }
 
-// s_waitcnt vmcnt(n) for a count known after unrolling (the switch folds)
+// s_waitcnt vmcnt(n) for a count known after unrolling (the switch folds; up to the 6-bit
+// field's 63, larger counts wait for everything)
 MLI_FI void vm_wait(int n) {
   switch (n) {
 #define MLI_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
     MLI_VMW(1) MLI_VMW(2) MLI_VMW(3) MLI_VMW(4) MLI_VMW(5) MLI_VMW(6) MLI_VMW(7) MLI_VMW(8)
     MLI_VMW(9) MLI_VMW(10) MLI_VMW(11) MLI_VMW(12) MLI_VMW(13) MLI_VMW(14) MLI_VMW(15) MLI_VMW(16)
+    MLI_VMW(17) MLI_VMW(18) MLI_VMW(19) MLI_VMW(20) MLI_VMW(21) MLI_VMW(22) MLI_VMW(23) MLI_VMW(24)
+    MLI_VMW(25) MLI_VMW(26) MLI_VMW(27) MLI_VMW(28) MLI_VMW(29) MLI_VMW(30) MLI_VMW(31) MLI_VMW(32)
+    MLI_VMW(33) MLI_VMW(34) MLI_VMW(35) MLI_VMW(36) MLI_VMW(37) MLI_VMW(38) MLI_VMW(39) MLI_VMW(40)
+    MLI_VMW(41) MLI_VMW(42) MLI_VMW(43) MLI_VMW(44) MLI_VMW(45) MLI_VMW(46) MLI_VMW(47) MLI_VMW(48)
+    MLI_VMW(49) MLI_VMW(50) MLI_VMW(51) MLI_VMW(52) MLI_VMW(53) MLI_VMW(54) MLI_VMW(55) MLI_VMW(56)
+    MLI_VMW(57) MLI_VMW(58) MLI_VMW(59) MLI_VMW(60) MLI_VMW(61) MLI_VMW(62) MLI_VMW(63)
 #undef MLI_VMW
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }

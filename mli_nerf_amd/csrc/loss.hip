@@ -143,12 +143,27 @@ __global__ __launch_bounds__(256) void terms_kernel(mli_loss_args a, int nb_ray)
   }
 }
 
-// thread i sums accumulator i over the workgroups, in workgroup order
-__global__ void finalize_kernel(mli_loss_args a, int n_blocks) {
+// thread i sums accumulator i over the workgroups, in workgroup order.  The partials come into
+// LDS by one coalesced pass of all threads first (a single thread walking them in global memory
+// paid one dependent load per workgroup: 30-125 us per step); the order of the adds is unchanged.
+constexpr int FIN_THREADS = 256;
+constexpr int FIN_MAX = 1024;  // workgroups whose partials fit the LDS copy (32 KiB)
+
+__global__ __launch_bounds__(FIN_THREADS) void finalize_kernel(mli_loss_args a, int n_blocks) {
+  __shared__ float part[FIN_MAX * ACC_N];
   __shared__ float acc[ACC_N];
+  const int n = n_blocks * ACC_N;
+  const bool staged = n_blocks <= FIN_MAX;
+  if (staged)
+    for (int e = threadIdx.x; e < n; e += FIN_THREADS) part[e] = a.scratch[4 + e];
+  __syncthreads();
   if (threadIdx.x < ACC_N) {
     float t = 0.f;
-    for (int b = 0; b < n_blocks; ++b) t += a.scratch[4 + (size_t)b * ACC_N + threadIdx.x];
+    if (staged) {
+      for (int b = 0; b < n_blocks; ++b) t += part[b * ACC_N + threadIdx.x];
+    } else {
+      for (int b = 0; b < n_blocks; ++b) t += a.scratch[4 + (size_t)b * ACC_N + threadIdx.x];
+    }
     acc[threadIdx.x] = t;
   }
   __syncthreads();
@@ -179,7 +194,7 @@ extern "C" int mli_stage_b_loss(const mli_loss_args* a, mli_stream_t s) {
   hipLaunchKernelGGL(minmax_kernel, dim3(1), dim3(1024), 0, (hipStream_t)s, *a);
   const int nb_ray = (a->R + 255) / 256;
   hipLaunchKernelGGL(terms_kernel, dim3(nb_ray + NB_SMP), dim3(256), 0, (hipStream_t)s, *a, nb_ray);
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)s, *a, n_blocks(a->R));
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(FIN_THREADS), 0, (hipStream_t)s, *a, n_blocks(a->R));
   MLI_LAUNCH_CHECK();
 }
 

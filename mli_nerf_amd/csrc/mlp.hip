@@ -4,7 +4,7 @@
 // LumenRGB.forward 'rgb_r_s' (NeuralLumen/utils/modules.py:148-163) with its three
 // MLPwithSkipConnection heads (nerf_util.py:158-196), and their autograd backward.
 //
-// Structure (one workgroup = 8 waves = 256 samples, one wave = 32 samples):
+// Structure (one workgroup = 8 waves = 256 samples, one wave = 32 samples; Geo below):
 //  * activations live in registers as MFMA B fragments of the transposed layer
 //    Y^T = W X^T (rows = features in the accumulator registers, samples on lanes), so the
 //    accumulator of layer l is the B operand of layer l+1 with no lane movement
@@ -24,22 +24,47 @@
 
 namespace {
 
-constexpr int THREADS = 512;
-constexpr int WAVES = 8;
 constexpr int CH(int ks) { return ks * 1024 + 128; }
 constexpr int FRAG_TILE = 16 * 64 * 8;  // halves per 32-sample tile of a 256-wide frag image
-// weight ring: NSLOT slots of 3 x 8 KiB (one 16 B LDS-DMA per thread per 8 KiB round)
-constexpr int GLDS = 3;
-constexpr int SLOT = GLDS * 8192;       // >= CH(19) = 19584
 constexpr int DIST = 2;                 // chunks in flight ahead of the one being read (3: no gain)
 constexpr int NSLOT = DIST + 1;
-// feature-major staging ([32 features][256 samples] fp16 per n-tile), double buffered
-constexpr int SROW = 256 * 2 + 16;      // 16 B pad
-constexpr int STAGE = 32 * SROW;
-constexpr int STAGE_OFF = NSLOT * SLOT;
-constexpr int MASK_OFF = STAGE_OFF + 2 * STAGE;  // backward: 2 x 8 KiB ReLU-mask blocks
-constexpr int LDS_FWD = STAGE_OFF + 2 * STAGE;
-constexpr int LDS_BWD = MASK_OFF + 2 * 8192;
+
+// Wave roles.  ALL: every wave issues its share of the weight DMAs and of the activation
+// flushes, and waits.  Split queues (DMA + STORE): vmcnt retires vector-memory ops in issue
+// order, so a wave that both streams weights and stores activations waits, for every weight
+// chunk, on the activation stores it issued before that chunk's DMAs.  The first half of the
+// waves (DMA) issue all the LDS-DMA (weights, ReLU masks) and are the only waves that wait on
+// vmcnt in the phase loop; the second half (STORE) issue all the activation flushes and never
+// wait on them.
+enum Role { ALL = 0, DMA = 1, STORE = 2 };
+
+// Workgroup geometry: NW waves of 32 samples (NW * 32 samples per workgroup), a weight ring of
+// NSLOT slots for chunks of up to MAXP 1 KiB pieces, split (DMA + STORE) or ALL wave roles.
+// The ring DMA of one chunk is ND waves x RND pieces of 1 KiB (16 B per lane); the
+// feature-major staging tile is [32 features][NW * 32 samples] fp16, double buffered; the
+// backward's ReLU-mask blocks are NW tiles x 1 KiB, double buffered.
+template <int NW_, int MAXP, bool SPLIT_>
+struct Geo {
+  static constexpr int NW = NW_;
+  static constexpr bool SPLIT = SPLIT_;
+  static constexpr int THREADS = NW * 64;
+  static constexpr int SAMPLES = NW * 32;
+  static constexpr int ND = SPLIT ? NW / 2 : NW;
+  static constexpr int RND = (MAXP + ND - 1) / ND;
+  static constexpr int SLOT = RND * ND * 1024;
+  static constexpr int SROW = SAMPLES * 2 + 16;  // 16 B pad
+  static constexpr int STAGE = 32 * SROW;
+  static constexpr int STAGE_OFF = NSLOT * SLOT;
+  static constexpr int MASKB = NW * 1024;
+  static constexpr int MASK_OFF = STAGE_OFF + 2 * STAGE;
+  static constexpr int LDS_FWD = STAGE_OFF + 2 * STAGE;
+  static constexpr int LDS_BWD = MASK_OFF + 2 * MASKB;
+  static constexpr int TPR = SAMPLES / 8;  // 16 B flush pieces per staged row
+  // ring DMAs per wave and chunk, flush stores per wave and staged tile
+  template <int ROLE> static constexpr int ring_ops() { return ROLE == STORE ? 0 : RND; }
+  template <int ROLE> static constexpr int flushers() { return ROLE == STORE ? THREADS / 2 : THREADS; }
+  template <int ROLE> static constexpr int flush_ops() { return ROLE == DMA ? 0 : 32 * TPR / flushers<ROLE>(); }
+};
 
 // ---------------------------------------------------------------------- weight ring
 struct Ring {
@@ -48,35 +73,25 @@ struct Ring {
   int next, n, cur;     // next chunk to issue, total chunks, chunk being consumed
 };
 
-// Wave roles.  ALL: every wave issues its share of the weight DMAs and of the activation
-// flushes, and waits.  Split queues (DMA + STORE): vmcnt retires vector-memory ops in issue
-// order, so a wave that both streams weights and stores activations waits, for every weight
-// chunk, on the activation stores it issued before that chunk's DMAs.  Waves 0-3 (DMA) issue
-// all the LDS-DMA (weights, ReLU masks) and are the only waves that wait on vmcnt in the
-// phase loop; waves 4-7 (STORE) issue all the activation flushes and never wait on them.
-enum Role { ALL = 0, DMA = 1, STORE = 2 };
-
 // The DMAs for chunk r.next into its slot (past the end: a dummy copy of the last chunk into a
-// free slot, so every phase issues the same count).  bytes(c) = size of chunk c.  ALL: GLDS
-// per wave (8 KiB rounds over 8 waves); DMA: 2 GLDS per wave (4 KiB rounds over 4 waves).
-template <int ROLE>
-constexpr int ring_ops() { return ROLE == ALL ? GLDS : ROLE == DMA ? 2 * GLDS : 0; }
-
-template <int ROLE, class Bytes>
-MLI_FI void ring_issue(Ring& r, uint8_t* lds, Bytes&& bytes) {
+// free slot, so every phase issues the same count).  bytes(c) = size of chunk c.  Piece
+// u * ND + wave of the chunk (1 KiB, lanes clamped to the chunk's last 16 B) goes to the same
+// offset of the slot.
+template <class G, int ROLE>
+MLI_FI void ring_pieces(const uint8_t* s, int nb, uint8_t* slot) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (ROLE != STORE) {
+#pragma unroll
+    for (int u = 0; u < G::RND; ++u)
+      glds16(s + min((u * G::ND + wave) * 1024 + lane * 16, nb - 16), slot + (u * G::ND + wave) * 1024);
+  }
+}
+
+template <class G, int ROLE, class Bytes>
+MLI_FI void ring_issue(Ring& r, uint8_t* lds, Bytes&& bytes) {
   const bool real = r.next < r.n;
   const int nb = bytes(real ? r.next : r.n - 1);
-  const uint8_t* s = real ? r.src : r.last;
-  uint8_t* dst = lds + (r.next % NSLOT) * SLOT + wave * 1024;
-  if (ROLE == ALL) {
-#pragma unroll
-    for (int u = 0; u < GLDS; ++u) glds16(s + min(u * 8192 + wave * 1024 + lane * 16, nb - 16), dst + u * 8192);
-  } else if (ROLE == DMA) {
-#pragma unroll
-    for (int u = 0; u < 2 * GLDS; ++u)
-      glds16(s + min(u * 4096 + wave * 1024 + lane * 16, nb - 16), dst + u * 4096);
-  }
+  ring_pieces<G, ROLE>(real ? r.src : r.last, nb, lds + (r.next % NSLOT) * G::SLOT);
   if (real) r.src += nb;
   r.next++;
 }
@@ -90,20 +105,9 @@ struct ChunkAt {
   MLI_FI int operator()(int) const { return CH(16); }
 };
 
-template <int ROLE>
+template <class G, int ROLE>
 MLI_FI void ring_issue(Ring& r, uint8_t* lds, ChunkAt& at) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint8_t* s = at.src(min(r.next, r.n - 1));
-  const int nb = CH(16);
-  uint8_t* dst = lds + (r.next % NSLOT) * SLOT + wave * 1024;
-  if (ROLE == ALL) {
-#pragma unroll
-    for (int u = 0; u < GLDS; ++u) glds16(s + min(u * 8192 + wave * 1024 + lane * 16, nb - 16), dst + u * 8192);
-  } else if (ROLE == DMA) {
-#pragma unroll
-    for (int u = 0; u < 2 * GLDS; ++u)
-      glds16(s + min(u * 4096 + wave * 1024 + lane * 16, nb - 16), dst + u * 4096);
-  }
+  ring_pieces<G, ROLE>(at.src(min(r.next, r.n - 1)), CH(16), lds + (r.next % NSLOT) * G::SLOT);
   r.next++;
 }
 
@@ -121,38 +125,44 @@ MLI_FI void ring_start(Ring& r, const void* base, int n, Bytes&& bytes) {
 // ---------------------------------------------------------------------- LDS staging
 // stage_tile() writes a feature-major tile (accumulator layout: rows acc_row(i, h), sample
 // column wave*32 + c) into one buffer; the next phase's barrier makes it visible and
-// stage_flush() writes it out (16 B per lane, 512 B per row) while the other buffer takes
+// stage_flush() writes it out (16 B per lane, NW * 64 B per row) while the other buffer takes
 // the next tile.
 struct Stager {
   uint16_t* pend;  // global address of (row 0, first sample of the block) of the staged tile
   int buf, pbuf;
 };
 
-MLI_FI void stage_tile(Stager& sg, uint8_t* lds, const f32x16& v, uint16_t* dst, int lane) {
+template <class G>
+MLI_FI void stage_tile(Stager& sg, uint8_t* lds, half8 f0, half8 f1, uint16_t* dst, int lane) {
+  // f0 / f1 = acc_to_frag(v, 0 / 1): element i of the tile is half (i & 1) of word (i & 7) >> 1
+  // of fragment i >> 3; it goes to row acc_row(i, h), column wave*32 + c
   const int wave = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
-  uint8_t* sb = lds + STAGE_OFF + sg.buf * STAGE + (4 * h) * SROW + (wave * 32 + c) * 2;
+  uint8_t* sb = lds + G::STAGE_OFF + sg.buf * G::STAGE + (4 * h) * G::SROW + (wave * 32 + c) * 2;
+  const u32x4 w[2] = {__builtin_bit_cast(u32x4, f0), __builtin_bit_cast(u32x4, f1)};
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const f16 x = (f16)v[i];
-    *reinterpret_cast<uint16_t*>(sb + ((i & 3) + 8 * (i >> 2)) * SROW) = __builtin_bit_cast(uint16_t, x);
+    const uint32_t word = w[i >> 3][(i & 7) >> 1];
+    *reinterpret_cast<uint16_t*>(sb + ((i & 3) + 8 * (i >> 2)) * G::SROW) =
+        (uint16_t)((i & 1) ? (word >> 16) : word);
   }
   sg.pend = dst;
   sg.pbuf = sg.buf;
   sg.buf ^= 1;
 }
 
-template <int ROLE>
+template <class G, int ROLE>
 MLI_FI void stage_flush(Stager& sg, const uint8_t* lds, int S) {
-  // ALL: 512 threads x 2 stores; STORE: waves 4-7, 256 threads x 4 stores; DMA: none
-  constexpr int NS = ROLE == ALL ? 2 : ROLE == STORE ? 4 : 0;
-  const int t = ROLE == STORE ? threadIdx.x - 256 : threadIdx.x;
-  const int row = t >> 5, col = t & 31;
-  const uint8_t* sb = lds + STAGE_OFF + sg.pbuf * STAGE + row * SROW + col * 16;
+  // ALL: every thread; STORE: the second half of the waves; DMA: none
+  constexpr int NS = G::template flush_ops<ROLE>();
+  constexpr int RSTEP = G::template flushers<ROLE>() / G::TPR;
+  const int t = ROLE == STORE ? threadIdx.x - G::THREADS / 2 : threadIdx.x;
+  const int row = t / G::TPR, col = t % G::TPR;
+  const uint8_t* sb = lds + G::STAGE_OFF + sg.pbuf * G::STAGE + row * G::SROW + col * 16;
   uint16_t* g = sg.pend + (size_t)row * S + col * 8;
-  const size_t step = (size_t)(32 / NS) * S;
+  const size_t step = (size_t)RSTEP * S;
 #pragma unroll
   for (int u = 0; u < NS; ++u) {
-    const u32x4 x = *reinterpret_cast<const u32x4*>(sb + (32 / NS) * u * SROW);
+    const u32x4 x = *reinterpret_cast<const u32x4*>(sb + RSTEP * u * G::SROW);
     // streaming (non-temporal) store: the activations are re-read only by a later kernel, so
     // they should not evict the weight chunks every phase re-reads from L2
     __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(g + u * step));
@@ -191,10 +201,10 @@ MLI_FI f32x16 chunk_mma(const uint8_t* chunk, const half8* X, int lane) {
 // EPI = unconditional global stores per epilogue, MASKED = one mask store at t == NT-1;
 // pre.issue(t) issues pre.count(t) VMEM ops ahead of the weight DMAs.  STORE waves never
 // wait in the loop: nothing they issue lands in LDS.
-template <int ROLE, int KS, int NT, bool STAGED, int EPI, bool MASKED, class Bytes, class Pre, class Epi>
+template <class G, int ROLE, int KS, int NT, bool STAGED, int EPI, bool MASKED, class Bytes, class Pre, class Epi>
 MLI_FI void run_layer(Ring& rg, uint8_t* lds, Stager& sg, int S, const half8* X, int lane, Bytes&& bytes,
                       Pre&& pre, Epi&& epi) {
-  constexpr int FL = ROLE == ALL ? 2 : 0;  // flush stores in this wave's queue
+  constexpr int FL = ROLE == ALL ? G::template flush_ops<ALL>() : 0;  // flush stores in this wave's queue
   // VMEM ops a phase issues after its weight DMAs (flush + epilogue stores), per t in the layer
   auto stores = [](int t) MLI_LAMBDA_FI {
     return ((t > 0 && STAGED) ? FL : 0) + EPI + ((MASKED && t == NT - 1) ? 1 : 0);
@@ -202,22 +212,22 @@ MLI_FI void run_layer(Ring& rg, uint8_t* lds, Stager& sg, int S, const half8* X,
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     pre.issue(t);
-    ring_issue<ROLE>(rg, lds, bytes);
+    ring_issue<G, ROLE>(rg, lds, bytes);
     if (ROLE != DMA) {
       if (t == 0) {
-        if (sg.pend) stage_flush<ROLE>(sg, lds, S);
+        if (sg.pend) stage_flush<G, ROLE>(sg, lds, S);
       } else if (STAGED) {
-        stage_flush<ROLE>(sg, lds, S);
+        stage_flush<G, ROLE>(sg, lds, S);
       }
     }
-    const f32x16 acc = chunk_mma<KS>(lds + (rg.cur % NSLOT) * SLOT, X, lane);
+    const f32x16 acc = chunk_mma<KS>(lds + (rg.cur % NSLOT) * G::SLOT, X, lane);
     epi(t, acc);
     // retire chunk cur+1 (its DMAs went out DIST-1 phases ago): every VMEM op issued after
     // them may stay in flight -- the weight DMAs of the DIST-1 later phases, the mask DMAs
     // and stores of this and the previous phases (counted inside this layer, lower bound 0
     // across the layer boundary)
     if (ROLE != STORE) {
-      int n = (DIST - 1) * ring_ops<ROLE>() + pre.count(t) + stores(t);
+      int n = (DIST - 1) * G::template ring_ops<ROLE>() + pre.count(t) + stores(t);
 #pragma unroll
       for (int b = 1; b < DIST; ++b) {
         if (t - b < 0) break;
@@ -240,12 +250,12 @@ struct NoPre {
 // L1..L3 (24 x KS 16), L4 (1 x KS 16)
 MLI_FI int fwd_bytes(int c) { return (c >= 8 && (c - 8) % 33 < 8) ? CH(19) : CH(16); }
 
-template <bool TRAIN, int ROLE>
+template <class G, bool TRAIN, int ROLE>
 MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int S = a.R * a.N;
-  const int tile = blockIdx.x * WAVES + wave;
+  const int tile = blockIdx.x * G::NW + wave;
   const int m = tile * 32 + c;
   const int r = m / a.N, k = m - r * a.N;
   const size_t slot = (size_t)k * a.R + r;
@@ -298,16 +308,16 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
   }
   // prologue: chunks 0 .. DIST-1 in flight, wait for chunk 0
 #pragma unroll
-  for (int d = 0; d < DIST; ++d) ring_issue<ROLE>(rg, lds, bytes);
-  if (ROLE != STORE) vm_wait((DIST - 1) * ring_ops<ROLE>());
+  for (int d = 0; d < DIST; ++d) ring_issue<G, ROLE>(rg, lds, bytes);
+  if (ROLE != STORE) vm_wait((DIST - 1) * G::template ring_ops<ROLE>());
   block_sync();
 
   Stager sg{nullptr, 0, 0};
-  const size_t col0 = (size_t)blockIdx.x * 256;
+  const size_t col0 = (size_t)blockIdx.x * G::SAMPLES;
 
   // SDF layer 1: feat = softplus(W1 h0 + b1) -> A; frag image scratch (+ x0T rows 0..255)
   uint16_t* ftile = a.feat_frag + (size_t)tile * FRAG_TILE;
-  run_layer<ROLE, 16, 8, TRAIN, 2, false>(rg, lds, sg, S, B, lane, bytes, NoPre{},
+  run_layer<G, ROLE, 16, 8, TRAIN, 2, false>(rg, lds, sg, S, B, lane, bytes, NoPre{},
                                     [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
     f32x16 v;
 #pragma unroll
@@ -317,7 +327,7 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
     half8* dst = reinterpret_cast<half8*>(ftile) + (2 * t) * 64 + lane;
     dst[0] = A[2 * t];
     dst[64] = A[2 * t + 1];
-    if (TRAIN) stage_tile(sg, lds, v, a.x0T + (size_t)(32 * t) * S + col0, lane);
+    if (TRAIN) stage_tile<G>(sg, lds, A[2 * t], A[2 * t + 1], a.x0T + (size_t)(32 * t) * S + col0, lane);
   });
 
   for (int hd = 0; hd < a.n_heads; ++hd) {
@@ -342,7 +352,8 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
 #pragma unroll
           for (int i = 0; i < 16; ++i) bits |= (acc[i] > 0.0f ? 1u : 0u) << i;
           if (t & 1) mbits[t >> 1] |= bits << 16; else mbits[t >> 1] = bits;
-          stage_tile(sg, lds, v, a.xT + ((size_t)(hd * 4 + layer) * 256 + 32 * t) * S + col0, lane);
+          stage_tile<G>(sg, lds, out[2 * t], out[2 * t + 1],
+                        a.xT + ((size_t)(hd * 4 + layer) * 256 + 32 * t) * S + col0, lane);
           if (t == 7) {
             u32x4* mp = reinterpret_cast<u32x4*>(a.masks) +
                         ((size_t)(hd * 4 + layer) * (S / 32) + tile) * 64 + lane;
@@ -351,13 +362,13 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
         }
       };
     };
-    run_layer<ROLE, 19, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, B, lane, bytes, NoPre{}, relu_epi(A, 0));
-    run_layer<ROLE, 16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, A, lane, bytes, NoPre{}, relu_epi(B, 1));
-    run_layer<ROLE, 16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, B, lane, bytes, NoPre{}, relu_epi(A, 2));
-    run_layer<ROLE, 16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, A, lane, bytes, NoPre{}, relu_epi(B, 3));
+    run_layer<G, ROLE, 19, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, B, lane, bytes, NoPre{}, relu_epi(A, 0));
+    run_layer<G, ROLE, 16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, A, lane, bytes, NoPre{}, relu_epi(B, 1));
+    run_layer<G, ROLE, 16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, B, lane, bytes, NoPre{}, relu_epi(A, 2));
+    run_layer<G, ROLE, 16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, A, lane, bytes, NoPre{}, relu_epi(B, 3));
     const int no = hd == 2 ? 1 : 3;
     const int off = hd * 3;
-    run_layer<ROLE, 16, 1, false, 0, false>(rg, lds, sg, S, B, lane, bytes, NoPre{},
+    run_layer<G, ROLE, 16, 1, false, 0, false>(rg, lds, sg, S, B, lane, bytes, NoPre{},
                                       [&](int, const f32x16& acc) MLI_LAMBDA_FI {
       if (h == 0) {
 #pragma unroll
@@ -369,12 +380,21 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
   vm_wait(0);  // no LDS-DMA may land after the workgroup's LDS is released
 }
 
-// waves 0-3 / 4-7 take the DMA / STORE roles (see Role), compiled as two programs
+// Heads kernels: 8 waves (256 samples) per workgroup, one workgroup per CU.  Measured against
+// 4 waves (128 samples, two independent workgroups per CU, so one workgroup's MFMAs could run
+// beside the other's epilogue): training forward 1.37 vs 1.29 ms, eval 0.88 vs 0.80 ms, rgb_bwd
+// 0.86 vs 0.81 ms -- the weight chunks stream through LDS once per workgroup, so halving the
+// workgroup doubles the ring DMA and LDS-write work per sample.
+typedef Geo<8, 20, true> GFwd;
+typedef Geo<8, 17, true> GBwd;
+
+// the first / second half of the waves take the DMA / STORE roles (see Role), compiled as two
+// programs
 template <bool TRAIN>
-__global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
+__global__ __launch_bounds__(GFwd::THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 8)) rgb_fwd_body<TRAIN, STORE>(a, lds);
-  else rgb_fwd_body<TRAIN, DMA>(a, lds);
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= GFwd::NW / 2) rgb_fwd_body<GFwd, TRAIN, STORE>(a, lds);
+  else rgb_fwd_body<GFwd, TRAIN, DMA>(a, lds);
 }
 
 // ---------------------------------------------------------------------- backward dX chain
@@ -382,42 +402,43 @@ __global__ __launch_bounds__(THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
 MLI_FI int bwd_bytes(int c) { return (c % 32) < 8 ? CH(1) : CH(16); }
 constexpr int BWD_CHUNKS = 3 * 32;
 
-template <int ROLE>
+template <class G, int ROLE>
 MLI_FI void rgb_bwd_body(const mli_rgb_bwd_args& a, uint8_t* lds) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int S = a.R * a.N;
   const int tiles = S / 32;
-  const int tile = blockIdx.x * WAVES + wave;
+  const int tile = blockIdx.x * G::NW + wave;
   const int m = tile * 32 + c;
   const int r = m / a.N, k = m - r * a.N;
   const size_t slot = (size_t)k * a.R + r;
   auto bytes = [](int cc) MLI_LAMBDA_FI { return bwd_bytes(cc); };
   // ReLU-mask block of global layer L (= head*4 + li, li = 0..3 runs masks 3, 2, 1, 0): the
-  // workgroup's 8 tiles are contiguous (8 KiB), DMA'd by the DMA waves (two 16 B per thread)
+  // workgroup's NW tiles are contiguous (NW KiB), DMA'd by the DMA waves (two 16 B per thread)
   // into mask slot L&1
-  constexpr int MASK_OPS = ROLE == DMA ? 2 : 0;
+  constexpr int MASK_OPS = ROLE == DMA ? 2 : ROLE == ALL ? 1 : 0;
   auto mask_dma = [&](int L) MLI_LAMBDA_FI {
     const int Lc = min(L, 11);
     const int hd = Lc >> 2, ml = 3 - (Lc & 3);
     const uint8_t* src = reinterpret_cast<const uint8_t*>(a.masks) +
-                         (((size_t)(hd * 4 + ml) * tiles + (size_t)blockIdx.x * WAVES) * 64) * 16;
+                         (((size_t)(hd * 4 + ml) * tiles + (size_t)blockIdx.x * G::NW) * 64) * 16;
 #pragma unroll
     for (int u = 0; u < MASK_OPS; ++u)
-      glds16(src + u * 4096 + threadIdx.x * 16, lds + MASK_OFF + (L & 1) * 8192 + u * 4096 + wave * 1024);
+      glds16(src + u * (G::MASKB / 2) + threadIdx.x * 16,
+             lds + G::MASK_OFF + (L & 1) * G::MASKB + u * (G::MASKB / 2) + wave * 1024);
   };
 
   Ring rg;
   ring_start(rg, a.wbwd, BWD_CHUNKS, bytes);
   mask_dma(0);
 #pragma unroll
-  for (int d = 0; d < DIST; ++d) ring_issue<ROLE>(rg, lds, bytes);
-  if (ROLE != STORE) vm_wait((DIST - 1) * ring_ops<ROLE>());
+  for (int d = 0; d < DIST; ++d) ring_issue<G, ROLE>(rg, lds, bytes);
+  if (ROLE != STORE) vm_wait((DIST - 1) * G::template ring_ops<ROLE>());
   block_sync();
 
   half8 A[16], B[16];
   Stager sg{nullptr, 0, 0};
-  const size_t col0 = (size_t)blockIdx.x * 256;
+  const size_t col0 = (size_t)blockIdx.x * G::SAMPLES;
   for (int hd = 0; hd < 3; ++hd) {
     const int S = opaque_s(a.R * a.N);
     const int no = hd == 2 ? 1 : 3;
@@ -450,7 +471,7 @@ MLI_FI void rgb_bwd_body(const mli_rgb_bwd_args& a, uint8_t* lds) {
     auto mask_epi = [&](half8* out, int layer /* dZ index */, int li) MLI_LAMBDA_FI {
       return [&, out, layer, li](int t, const f32x16& acc) MLI_LAMBDA_FI {
         const u32x4 mv =
-            *reinterpret_cast<const u32x4*>(lds + MASK_OFF + (li & 1) * 8192 + wave * 1024 + lane * 16);
+            *reinterpret_cast<const u32x4*>(lds + G::MASK_OFF + (li & 1) * G::MASKB + wave * 1024 + lane * 16);
         const int wi = t >> 1;
         const uint32_t word = wi == 0 ? mv[0] : wi == 1 ? mv[1] : wi == 2 ? mv[2] : mv[3];
         const uint32_t bits = word >> ((t & 1) * 16);
@@ -459,23 +480,24 @@ MLI_FI void rgb_bwd_body(const mli_rgb_bwd_args& a, uint8_t* lds) {
         for (int i = 0; i < 16; ++i) v[i] = ((bits >> i) & 1u) ? acc[i] : 0.0f;
         out[2 * t] = acc_to_frag(v, 0);
         out[2 * t + 1] = acc_to_frag(v, 1);
-        stage_tile(sg, lds, v, a.dzT + ((size_t)(hd * 4 + layer) * 256 + 32 * t) * S + col0, lane);
+        stage_tile<G>(sg, lds, out[2 * t], out[2 * t + 1],
+                      a.dzT + ((size_t)(hd * 4 + layer) * 256 + 32 * t) * S + col0, lane);
       };
     };
-    run_layer<ROLE, 1, 8, true, 0, false>(rg, lds, sg, S, &z4, lane, bytes, pre(0), mask_epi(A, 3, 0));
-    run_layer<ROLE, 16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, pre(1), mask_epi(B, 2, 1));
-    run_layer<ROLE, 16, 8, true, 0, false>(rg, lds, sg, S, B, lane, bytes, pre(2), mask_epi(A, 1, 2));
-    run_layer<ROLE, 16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, pre(3), mask_epi(B, 0, 3));
+    run_layer<G, ROLE, 1, 8, true, 0, false>(rg, lds, sg, S, &z4, lane, bytes, pre(0), mask_epi(A, 3, 0));
+    run_layer<G, ROLE, 16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, pre(1), mask_epi(B, 2, 1));
+    run_layer<G, ROLE, 16, 8, true, 0, false>(rg, lds, sg, S, B, lane, bytes, pre(2), mask_epi(A, 1, 2));
+    run_layer<G, ROLE, 16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, pre(3), mask_epi(B, 0, 3));
   }
   // the last tile, made visible by the last phase's barrier
-  stage_flush<ROLE>(sg, lds, opaque_s(a.R * a.N));
+  stage_flush<G, ROLE>(sg, lds, opaque_s(a.R * a.N));
   vm_wait(0);
 }
 
-__global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
+__global__ __launch_bounds__(GBwd::THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 8)) rgb_bwd_body<STORE>(a, lds);
-  else rgb_bwd_body<DMA>(a, lds);
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= GBwd::NW / 2) rgb_bwd_body<GBwd, STORE>(a, lds);
+  else rgb_bwd_body<GBwd, DMA>(a, lds);
 }
 
 
@@ -486,21 +508,25 @@ __global__ __launch_bounds__(THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
 // the layer-0 dW).  One workgroup = 256 samples, as mli_rgb_bwd.
 constexpr int HB_HEAD_BYTES = 8 * CH(1) + 24 * CH(16);
 
+typedef Geo<8, 17, true> GDz0;
+
 template <int ROLE>
 MLI_FI void dz0_body(const mli_heads_bwd_args& a, uint8_t* lds) {
+  typedef GDz0 G;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int tiles = a.R * a.N / 32;
-  const int tile = blockIdx.x * WAVES + wave;
+  const int tile = blockIdx.x * G::NW + wave;
   ChunkAt at{reinterpret_cast<const uint8_t*>(a.wbwd), HB_HEAD_BYTES, 8 * CH(1) + 16 * CH(16)};
   constexpr int MASK_OPS = ROLE == DMA ? 2 : 0;
   // ReLU masks of head layer 0 of head hd (the workgroup's 8 tiles, 8 KiB) into slot hd & 1
   auto mask_dma = [&](int hd) MLI_LAMBDA_FI {
     const int hc = min(hd, 2);
     const uint8_t* src = reinterpret_cast<const uint8_t*>(a.masks) +
-                         (((size_t)(hc * 4) * tiles + (size_t)blockIdx.x * WAVES) * 64) * 16;
+                         (((size_t)(hc * 4) * tiles + (size_t)blockIdx.x * G::NW) * 64) * 16;
 #pragma unroll
     for (int u = 0; u < MASK_OPS; ++u)
-      glds16(src + u * 4096 + threadIdx.x * 16, lds + MASK_OFF + (hd & 1) * 8192 + u * 4096 + wave * 1024);
+      glds16(src + u * (G::MASKB / 2) + threadIdx.x * 16,
+             lds + G::MASK_OFF + (hd & 1) * G::MASKB + u * (G::MASKB / 2) + wave * 1024);
   };
   Ring rg;
   rg.src = rg.last = nullptr;
@@ -509,13 +535,13 @@ MLI_FI void dz0_body(const mli_heads_bwd_args& a, uint8_t* lds) {
   rg.cur = 0;
   mask_dma(0);
 #pragma unroll
-  for (int d = 0; d < DIST; ++d) ring_issue<ROLE>(rg, lds, at);
-  if (ROLE != STORE) vm_wait((DIST - 1) * ring_ops<ROLE>());
+  for (int d = 0; d < DIST; ++d) ring_issue<G, ROLE>(rg, lds, at);
+  if (ROLE != STORE) vm_wait((DIST - 1) * G::template ring_ops<ROLE>());
   block_sync();
 
   half8 B[16];
   Stager sg{nullptr, 0, 0};
-  const size_t col0 = (size_t)blockIdx.x * 256;
+  const size_t col0 = (size_t)blockIdx.x * G::SAMPLES;
   for (int hd = 0; hd < 3; ++hd) {
     const int S = opaque_s(a.R * a.N);
     {
@@ -532,24 +558,25 @@ MLI_FI void dz0_body(const mli_heads_bwd_args& a, uint8_t* lds) {
         if (t == 8 - DIST) dma(next_head);
       }
     };
-    run_layer<ROLE, 16, 8, true, 0, false>(rg, lds, sg, S, B, lane, at, MaskPre{mask_dma, hd + 1},
+    run_layer<G, ROLE, 16, 8, true, 0, false>(rg, lds, sg, S, B, lane, at, MaskPre{mask_dma, hd + 1},
                                           [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
       const u32x4 mv =
-          *reinterpret_cast<const u32x4*>(lds + MASK_OFF + (hd & 1) * 8192 + wave * 1024 + lane * 16);
+          *reinterpret_cast<const u32x4*>(lds + G::MASK_OFF + (hd & 1) * G::MASKB + wave * 1024 + lane * 16);
       const int wi = t >> 1;
       const uint32_t word = wi == 0 ? mv[0] : wi == 1 ? mv[1] : wi == 2 ? mv[2] : mv[3];
       const uint32_t bits = word >> ((t & 1) * 16);
       f32x16 v;
 #pragma unroll
       for (int i = 0; i < 16; ++i) v[i] = ((bits >> i) & 1u) ? acc[i] : 0.0f;
-      stage_tile(sg, lds, v, a.dz0T + ((size_t)hd * 256 + 32 * t) * S + col0, lane);
+      stage_tile<G>(sg, lds, acc_to_frag(v, 0), acc_to_frag(v, 1), a.dz0T + ((size_t)hd * 256 + 32 * t) * S + col0,
+                    lane);
     });
   }
-  stage_flush<ROLE>(sg, lds, opaque_s(a.R * a.N));
+  stage_flush<G, ROLE>(sg, lds, opaque_s(a.R * a.N));
   vm_wait(0);
 }
 
-__global__ __launch_bounds__(THREADS) void dz0_kernel(mli_heads_bwd_args a) {
+__global__ __launch_bounds__(GDz0::THREADS) void dz0_kernel(mli_heads_bwd_args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 8)) dz0_body<STORE>(a, lds);
   else dz0_body<DMA>(a, lds);
@@ -562,13 +589,16 @@ __global__ __launch_bounds__(THREADS) void dz0_kernel(mli_heads_bwd_args a) {
 MLI_FI int geo_bytes(int c) { return c < 8 ? CH(1) : CH(16); }
 constexpr int GEO_CHUNKS = 8 + 24 + 9 + 8;
 
-__global__ __launch_bounds__(THREADS) void geo_bwd_kernel(mli_geo_bwd_args a) {
+typedef Geo<8, 17, false> GGeo;
+
+__global__ __launch_bounds__(GGeo::THREADS) void geo_bwd_kernel(mli_geo_bwd_args a) {
+  typedef GGeo G;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
   const int S = a.R * a.N;
   const int tiles = S / 32;
-  const int tile = blockIdx.x * WAVES + wave;
+  const int tile = blockIdx.x * G::NW + wave;
   const int m = tile * 32 + c;
   const int r = m / a.N, k = m - r * a.N;
   const size_t slot = (size_t)k * a.R + r;
@@ -577,21 +607,21 @@ __global__ __launch_bounds__(THREADS) void geo_bwd_kernel(mli_geo_bwd_args a) {
   auto mask_dma = [&](int L) MLI_LAMBDA_FI {
     const int ml = 3 - min(L, 3);
     const uint8_t* src = reinterpret_cast<const uint8_t*>(a.masks) +
-                         (((size_t)ml * tiles + (size_t)blockIdx.x * WAVES) * 64) * 16;
-    glds16(src + threadIdx.x * 16, lds + MASK_OFF + (L & 1) * 8192 + wave * 1024);
+                         (((size_t)ml * tiles + (size_t)blockIdx.x * G::NW) * 64) * 16;
+    glds16(src + threadIdx.x * 16, lds + G::MASK_OFF + (L & 1) * G::MASKB + wave * 1024);
   };
 
   Ring rg;
   ring_start(rg, a.wgeo, GEO_CHUNKS, bytes);
   mask_dma(0);
 #pragma unroll
-  for (int d = 0; d < DIST; ++d) ring_issue<ALL>(rg, lds, bytes);
-  vm_wait((DIST - 1) * GLDS);
+  for (int d = 0; d < DIST; ++d) ring_issue<G, ALL>(rg, lds, bytes);
+  vm_wait((DIST - 1) * G::template ring_ops<ALL>());
   block_sync();
 
   half8 A[16], B[16];
   Stager sg{nullptr, 0, 0};
-  const size_t col0 = (size_t)blockIdx.x * 256;
+  const size_t col0 = (size_t)blockIdx.x * G::SAMPLES;
   half8 z4;
   {
     const float* dz = a.dz4 + 8 * slot;
@@ -618,7 +648,7 @@ __global__ __launch_bounds__(THREADS) void geo_bwd_kernel(mli_geo_bwd_args a) {
   auto mask_epi = [&](half8* out, int layer, int li) MLI_LAMBDA_FI {
     return [&, out, layer, li](int t, const f32x16& acc) MLI_LAMBDA_FI {
       const u32x4 mv =
-          *reinterpret_cast<const u32x4*>(lds + MASK_OFF + (li & 1) * 8192 + wave * 1024 + lane * 16);
+          *reinterpret_cast<const u32x4*>(lds + G::MASK_OFF + (li & 1) * G::MASKB + wave * 1024 + lane * 16);
       const int wi = t >> 1;
       const uint32_t word = wi == 0 ? mv[0] : wi == 1 ? mv[1] : wi == 2 ? mv[2] : mv[3];
       const uint32_t bits = word >> ((t & 1) * 16);
@@ -627,13 +657,13 @@ __global__ __launch_bounds__(THREADS) void geo_bwd_kernel(mli_geo_bwd_args a) {
       for (int i = 0; i < 16; ++i) v[i] = ((bits >> i) & 1u) ? acc[i] : 0.0f;
       out[2 * t] = acc_to_frag(v, 0);
       out[2 * t + 1] = acc_to_frag(v, 1);
-      stage_tile(sg, lds, v, a.dzT + ((size_t)layer * 256 + 32 * t) * S + col0, lane);
+      stage_tile<G>(sg, lds, out[2 * t], out[2 * t + 1], a.dzT + ((size_t)layer * 256 + 32 * t) * S + col0, lane);
     };
   };
-  run_layer<ALL, 1, 8, true, 0, false>(rg, lds, sg, S, &z4, lane, bytes, pre(0), mask_epi(A, 3, 0));
-  run_layer<ALL, 16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, pre(1), mask_epi(B, 2, 1));
-  run_layer<ALL, 16, 8, true, 0, false>(rg, lds, sg, S, B, lane, bytes, pre(2), mask_epi(A, 1, 2));
-  run_layer<ALL, 16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, NoPre{}, mask_epi(B, 0, 3));
+  run_layer<G, ALL, 1, 8, true, 0, false>(rg, lds, sg, S, &z4, lane, bytes, pre(0), mask_epi(A, 3, 0));
+  run_layer<G, ALL, 16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, pre(1), mask_epi(B, 2, 1));
+  run_layer<G, ALL, 16, 8, true, 0, false>(rg, lds, sg, S, B, lane, bytes, pre(2), mask_epi(A, 1, 2));
+  run_layer<G, ALL, 16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, NoPre{}, mask_epi(B, 0, 3));
   // feat frags (softplus output of SDF layer 1, forward scratch), one tile ahead of its use:
   // tile 0 now, tile t+1 ahead of phase t's weight DMAs (counted as pre-issued VMEM ops)
   const half8* fsrc = reinterpret_cast<const half8*>(a.feat_frag + (size_t)tile * FRAG_TILE) + lane;
@@ -654,7 +684,7 @@ __global__ __launch_bounds__(THREADS) void geo_bwd_kernel(mli_geo_bwd_args a) {
   // dX0 = W0^T dZ0: tiles 0..7 = d feat -> dZ1sdf = d feat * softplus'(z1), with
   // softplus'(z1) = 1 - exp(-100 feat) (torch: z/(z+1), z = e^{100 z1}; 1 past the threshold);
   // tile 8 = rows 256..287 (p 256..258, normal 259..261: (i=3,h=0), (i=0,h=1), (i=1,h=1))
-  run_layer<ALL, 16, 9, true, 0, false>(rg, lds, sg, S, B, lane, bytes, FeatPre{fsrc, F},
+  run_layer<G, ALL, 16, 9, true, 0, false>(rg, lds, sg, S, B, lane, bytes, FeatPre{fsrc, F},
                                    [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
     if (t < 8) {
       f32x16 v;
@@ -667,7 +697,7 @@ __global__ __launch_bounds__(THREADS) void geo_bwd_kernel(mli_geo_bwd_args a) {
         }
       A[2 * t] = acc_to_frag(v, 0);
       A[2 * t + 1] = acc_to_frag(v, 1);
-      stage_tile(sg, lds, v, a.dz1T + (size_t)(32 * t) * S + col0, lane);
+      stage_tile<G>(sg, lds, A[2 * t], A[2 * t + 1], a.dz1T + (size_t)(32 * t) * S + col0, lane);
     } else {
       float* dn = a.d_nrm + 4 * slot;
       if (h == 0) {
@@ -680,7 +710,7 @@ __global__ __launch_bounds__(THREADS) void geo_bwd_kernel(mli_geo_bwd_args a) {
   });
   // d h0 (layer-1 path) = W1sdf^T dZ1sdf -> frag image (ACC order, as the h0 image)
   uint16_t* dtile = a.dh0_frag + (size_t)tile * FRAG_TILE;
-  run_layer<ALL, 16, 8, false, 2, false>(rg, lds, sg, S, A, lane, bytes, NoPre{},
+  run_layer<G, ALL, 16, 8, false, 2, false>(rg, lds, sg, S, A, lane, bytes, NoPre{},
                                     [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
     half8* dst = reinterpret_cast<half8*>(dtile) + (2 * t) * 64 + lane;
     __builtin_nontemporal_store(acc_to_frag(acc, 0), dst);
@@ -695,7 +725,7 @@ namespace mli_detail {
 int heads_dz0_launch(const mli_heads_bwd_args* a, hipStream_t s) {
   const int S = a->R * a->N;
   if (S % 256 != 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(dz0_kernel, dim3(S / 256), dim3(THREADS), LDS_BWD, s, *a);
+  hipLaunchKernelGGL(dz0_kernel, dim3(S / GDz0::SAMPLES), dim3(GDz0::THREADS), GDz0::LDS_BWD, s, *a);
   return (int)hipGetLastError();
 }
 }  // namespace mli_detail
@@ -707,16 +737,19 @@ extern "C" int mli_rgb_fwd(const mli_rgb_fwd_args* a, mli_stream_t s) {
   if (train && (a->x0T == nullptr || a->masks == nullptr)) return (int)hipErrorInvalidValue;
   if (a->n_heads != 1 && a->n_heads != 3) return (int)hipErrorInvalidValue;
   if (train)
-    hipLaunchKernelGGL(rgb_fwd_kernel<true>, dim3(S / 256), dim3(THREADS), LDS_FWD, (hipStream_t)s, *a);
+    hipLaunchKernelGGL(rgb_fwd_kernel<true>, dim3(S / GFwd::SAMPLES), dim3(GFwd::THREADS), GFwd::LDS_FWD,
+                       (hipStream_t)s, *a);
   else
-    hipLaunchKernelGGL(rgb_fwd_kernel<false>, dim3(S / 256), dim3(THREADS), LDS_FWD, (hipStream_t)s, *a);
+    hipLaunchKernelGGL(rgb_fwd_kernel<false>, dim3(S / GFwd::SAMPLES), dim3(GFwd::THREADS), GFwd::LDS_FWD,
+                       (hipStream_t)s, *a);
   MLI_LAUNCH_CHECK();
 }
 
 extern "C" int mli_rgb_bwd(const mli_rgb_bwd_args* a, mli_stream_t s) {
   const int S = a->R * a->N;
   if (S % 256 != 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(rgb_bwd_kernel, dim3(S / 256), dim3(THREADS), LDS_BWD, (hipStream_t)s, *a);
+  hipLaunchKernelGGL(rgb_bwd_kernel, dim3(S / GBwd::SAMPLES), dim3(GBwd::THREADS), GBwd::LDS_BWD, (hipStream_t)s,
+                     *a);
   MLI_LAUNCH_CHECK();
 }
 
@@ -757,6 +790,7 @@ extern "C" int mli_geo_bwd(const mli_geo_bwd_args* a, mli_stream_t s) {
   if (!a->dz4 || !a->wgeo || !a->masks || !a->feat_frag || !a->dzT || !a->dz4T || !a->d_nrm || !a->dz1T ||
       !a->dh0_frag)
     return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(geo_bwd_kernel, dim3(S / 256), dim3(THREADS), LDS_BWD, (hipStream_t)s, *a);
+  hipLaunchKernelGGL(geo_bwd_kernel, dim3(S / GGeo::SAMPLES), dim3(GGeo::THREADS), GGeo::LDS_BWD, (hipStream_t)s,
+                     *a);
   MLI_LAUNCH_CHECK();
 }

@@ -200,6 +200,7 @@ class Trainer:
         # heads forward of the last train_step) or "wgrad" (after its heads backward); with
         # the last two, prefetch is called after train_step
         self.prefetch_gate = "call"
+        self.side_priority = 0  # torch stream priority of the prefetch stream (lower = higher)
         self._gate_ev = None
         self.sched = o.sched
         self.current_iteration = 0
@@ -298,7 +299,7 @@ class Trainer:
         dev = m.flat.device
         main = torch.cuda.current_stream(dev)
         if self._side is None or self._side.device != dev:
-            self._side = torch.cuda.Stream(device=dev)
+            self._side = torch.cuda.Stream(device=dev, priority=self.side_priority)
         ready = self._gate_ev if self.prefetch_gate != "call" else None
         if ready is None:
             ready = torch.cuda.Event()
