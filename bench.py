@@ -374,6 +374,9 @@ def main():
     ap.add_argument("--priority", choices=("none", "main", "side"), default="none",
                     help="pipeline: run the step on a high-priority stream (main) or give the prefetch "
                          "stream the high priority (side)")
+    ap.add_argument("--tail", choices=("fused", "three"), default="fused",
+                    help="stage-b training tail: fused (mli_composite_loss, one launch) or the three calls "
+                         "mli_composite_fwd / mli_stage_b_loss / mli_composite_bwd")
     ap.add_argument("--heads-bwd", choices=("fused", "split"), default="split",
                     help="stage-b heads backward: fused (mli_heads_bwd: dX chain + 256x256 dW in one launch) "
                          "or split (mli_rgb_bwd + mli_wgrad BIG)")
@@ -418,6 +421,7 @@ def main():
     model.load_state_dict(synthetic.make_state_dict(log2T=22, seed=0, heads="rgb" if stage_a else "rgb_r_s"))
     model = model.to(dev)
     trainer = Trainer(cfg, is_inference=False, model=model, world_size=world)
+    trainer.fused_tail = args.tail == "fused"
     model.heads_bwd = args.heads_bwd
     model.heads_split = tuple(int(x) for x in args.heads_split.split(","))
     if stage_a:
@@ -528,7 +532,7 @@ def main():
         "config": {"workload": "%s stage-%s train step" % (args.config, model.stage), "rays_per_gpu": R,
                    "samples_per_ray": N, "global_rays": R * world, "image": [Hh, W], "parallelism": "dp%d" % world,
                    "pipeline": ("geometry prefetch on a side stream, gate " + args.pipeline) if pipe else "off",
-                   "heads_bwd": args.heads_bwd},
+                   "heads_bwd": args.heads_bwd, "tail": args.tail},
         "kernel_timing": ("HIP events on the launch stream over %d extra steps with the prefetch off" % k_steps)
         if pipe else "HIP events on the launch stream over the timed steps",
         "psnr": round(psnr, 4), "loss": round(loss, 6),

@@ -44,7 +44,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mli_stream_t; /* == hipStream_t */
 
-#define MLI_ABI_VERSION 9
+#define MLI_ABI_VERSION 10
 #define MLI_HIDDEN 256
 #define MLI_LEVELS 16
 #define MLI_LEVEL_FEAT 8
@@ -494,6 +494,25 @@ int mli_stage_b_loss(const mli_loss_args* a, mli_stream_t s);
 /* bytes[0]: scratch; bytes[1..4]: d_rgb, d_o_r, d_o_s, d_o_re. */
 int mli_stage_b_loss_workspace(const mli_loss_args* a, int64_t* bytes);
 
+/* ---------------------------------------------------------------- fused training tail
+ * mli_composite_fwd (training outputs) + mli_stage_b_loss + mli_composite_bwd in one launch,
+ * one wave per ray (the fused stage-b train step), plus a one-workgroup launch that sums the
+ * loss partials: the composited outputs and the loss gradients stay in registers.  Outputs
+ * (weights, rgb, o_r, o_s, o_re) and dz4 equal the three-call path bit for bit (one definition
+ * of each formula); the loss values are the same sums in another fixed order, so repeated
+ * calls are bit-identical.
+ * Replaces the same reference functions as those three calls. */
+typedef struct {
+  mli_composite_args comp; /* opacity, gradient, depth, blend_dist: ignored (training)          */
+  mli_loss_args loss;      /* rgb, o_r, o_s, o_re, d_rgb, d_o_r, d_o_s, d_o_re: ignored;
+                              scratch = workspace bytes[0] (no zeroing needed)                  */
+  float grad_scale;        /* as mli_composite_bwd_args */
+  float* dz4;              /* [N][R][8], as mli_composite_bwd_args */
+} mli_composite_loss_args;
+int mli_composite_loss(const mli_composite_loss_args* a, mli_stream_t s);
+/* bytes[0]: scratch (workgroup partials); bytes[1]: dz4. */
+int mli_composite_loss_workspace(const mli_composite_loss_args* a, int64_t* bytes);
+
 /* ---------------------------------------------------------------- parameters
  * Weight-norm W = g * v / ||v||_row (torch.nn.utils.weight_norm dim=0) folded once per
  * step and packed into the fp16 MFMA chunk images the kernels stream; layer descriptors
@@ -563,6 +582,11 @@ int mli_adamw(const mli_adamw_args* a, mli_stream_t s);
 /* fp32 -> fp16 copy (hash-table shadow). */
 typedef struct { const float* src; uint16_t* dst; int64_t n; } mli_cast_args;
 int mli_cast_f16(const mli_cast_args* a, mli_stream_t s);
+
+/* sha256 prefix (16 hex digits) of the sources and compile flags this library was built from
+ * (mli_nerf_amd/build.py source_hash): the Python host refuses a library whose hash differs
+ * from its in-tree sources. */
+const char* mli_source_hash(void);
 
 #ifdef __cplusplus
 }

@@ -97,6 +97,10 @@ class LossArgs(C.Structure):
                 ("scratch", P)]
 
 
+
+class CompositeLossArgs(C.Structure):
+    _fields_ = [("comp", CompositeArgs), ("loss", LossArgs), ("grad_scale", F32), ("dz4", P)]
+
 class PackLayer(C.Structure):
     _fields_ = [("v", P), ("g", P), ("bias", P), ("n_out", I32), ("k_ref", I32), ("transpose", I32),
                 ("n_tiles", I32), ("k_steps", I32), ("kmap", P), ("kmode", P), ("dst_offset", I64),
@@ -180,7 +184,7 @@ class FragRowsArgs(C.Structure):
                 ("ld", I64), ("col0", I64), ("row0", I32)]
 
 
-ABI_VERSION = 9  # include/mli_hip.h MLI_ABI_VERSION
+ABI_VERSION = 10  # include/mli_hip.h MLI_ABI_VERSION
 
 ENTRY_POINTS = {
     "mli_rays": RaysArgs, "mli_hashgrid_fwd": HashgridArgs, "mli_sdf": SdfArgs,
@@ -193,6 +197,7 @@ ENTRY_POINTS = {
     "mli_composite_bwd_geo": CompositeBwdGeoArgs, "mli_geo_bwd": GeoBwdArgs, "mli_sdf_bwd": SdfBwdArgs,
     "mli_pack_sdf_t": PackSdfTArgs, "mli_hash_bwd": HashBwdArgs, "mli_frag_rows": FragRowsArgs,
     "mli_light_visibility": LightVisibilityArgs, "mli_ray_batch": RayBatchArgs,
+    "mli_composite_loss": CompositeLossArgs,
 }
 
 # host-only scratch-size queries: int mli_<op>_workspace(const args*, int64_t* bytes) -> how many
@@ -200,7 +205,7 @@ ENTRY_POINTS = {
 WORKSPACE = {
     "mli_sdf": 1, "mli_rgb_fwd": 5, "mli_rgb_bwd": 2, "mli_wgrad": 1, "mli_composite_bwd_geo": 4,
     "mli_geo_bwd": 6, "mli_sdf_bwd": 4, "mli_hash_bwd": 1, "mli_light_visibility": 5, "mli_stage_b_loss": 5,
-    "mli_pack": 1, "mli_heads_bwd": 4,
+    "mli_pack": 1, "mli_heads_bwd": 4, "mli_composite_loss": 2,
 }
 
 _lib = None
@@ -224,8 +229,15 @@ def lib():
         _lib.mli_abi_version.restype = I32
         _lib.mli_error_string.restype = C.c_char_p
         _lib.mli_error_string.argtypes = [I32]
+        _lib.mli_source_hash.restype = C.c_char_p
         if _lib.mli_abi_version() != ABI_VERSION:
             raise ImportError("libmli_hip.so ABI mismatch")
+        from . import build as _build
+        if all(os.path.exists(d) for d in _build._deps()):  # in-tree sources: the library must match
+            want, got = _build.source_hash(), _lib.mli_source_hash().decode()
+            if got != want:
+                raise ImportError("libmli_hip.so is stale (built from sources %s, the tree is %s); rebuild with "
+                                  "mli_nerf_amd.build.build()" % (got, want))
     return _lib
 
 

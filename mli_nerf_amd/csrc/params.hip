@@ -189,4 +189,11 @@ extern "C" int mli_cast_f16(const mli_cast_args* a, mli_stream_t s) {
 
 extern "C" int mli_abi_version(void) { return MLI_ABI_VERSION; }
 
+#ifndef MLI_SOURCE_HASH
+#define MLI_SOURCE_HASH "unknown"
+#endif
+// build.py's sha256 of the sources + flags, behind a marker it finds in the file without loading it
+static const char mli_source_hash_tag[] __attribute__((used)) = "MLI_SOURCE_HASH=" MLI_SOURCE_HASH;
+extern "C" const char* mli_source_hash(void) { return mli_source_hash_tag + 16; }
+
 extern "C" const char* mli_error_string(int code) { return hipGetErrorString((hipError_t)code); }

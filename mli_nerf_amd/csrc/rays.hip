@@ -6,6 +6,7 @@
 // (cumprod / cumsum) keep the reference's left-to-right accumulation order.
 // Compiled with -ffp-contract=off: products and sums round like the reference's torch ops.
 #include "common.h"
+#include "loss.h"
 
 namespace {
 
@@ -263,22 +264,23 @@ __global__ __launch_bounds__(FW * 64) void sample_fine_kernel(FineArgs fa) {
 // (neuralangelo/model.py:492-515), exclusive transmittance by a wave product scan
 // (render.py:87-99), the composited sums by wave reductions (NeuralLumen/model.py:266-305).
 constexpr int CW = 4;  // rays per block
-__global__ __launch_bounds__(CW * 64) void composite_fwd_kernel(mli_composite_args a) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+constexpr int CE = 4;  // samples per lane
+
+// The ray's NeuS alphas, weights (stored) and the wave-reduced composited sums acc[12]
+// (rgb 3, o_r 3, o_s, opacity, gradient 3, sum w d), every lane holding lane 0's values.
+// yk: the head outputs each lane read for its samples (kept for the fused backward).
+MLI_FI void composite_ray(const mli_composite_args& a, int r, int lane, float (&wv)[CE], float (&yk)[CE][7],
+                          float (&acc)[12]) {
   const int R = a.R, N = a.N;
-  const int rr = blockIdx.x * CW + w;
-  if (rr >= R) return;  // whole wave exits (no block barriers below)
-  const int r = rr;
   const float inv_s = expf(a.s_var[0]);
   const float an = a.anneal;
   const float v0 = a.ray_unit[3 * r], v1 = a.ray_unit[3 * r + 1], v2 = a.ray_unit[3 * r + 2];
   const float far = a.far_[r];
-  constexpr int E = 4;
-  float al[E], dk[E], g[E][3], wv[E];
+  float al[CE], dk[CE], g[CE][3];
   float lp = 1.f;
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const int k = E * lane + e;
+  for (int e = 0; e < CE; ++e) {
+    const int k = CE * lane + e;
     al[e] = 0.f; dk[e] = 0.f; g[e][0] = g[e][1] = g[e][2] = 0.f;
     if (k < N) {
       const size_t s = (size_t)k * R + r;
@@ -300,19 +302,22 @@ __global__ __launch_bounds__(CW * 64) void composite_fwd_kernel(mli_composite_ar
     lp *= 1.0f - al[e];
   }
   float T = wave_excl_prod(lp, lane);
-  float acc[12];
 #pragma unroll
   for (int i = 0; i < 12; ++i) acc[i] = 0.f;
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const int k = E * lane + e;
+  for (int e = 0; e < CE; ++e) {
+    const int k = CE * lane + e;
     wv[e] = al[e] * T;
     T = T * (1.0f - al[e]);
+#pragma unroll
+    for (int i = 0; i < 7; ++i) yk[e][i] = 0.f;
     if (k < N) {
       const size_t s = (size_t)k * R + r;
       a.weights[s] = wv[e];
       const f32x4 y0 = *reinterpret_cast<const f32x4*>(a.y + 8 * s);
       const f32x4 y1 = *reinterpret_cast<const f32x4*>(a.y + 8 * s + 4);
+      yk[e][0] = y0[0]; yk[e][1] = y0[1]; yk[e][2] = y0[2]; yk[e][3] = y0[3];
+      yk[e][4] = y1[0]; yk[e][5] = y1[1]; yk[e][6] = y1[2];
       acc[0] += y0[0] * wv[e]; acc[1] += y0[1] * wv[e]; acc[2] += y0[2] * wv[e];
       acc[3] += y0[3] * wv[e]; acc[4] += y1[0] * wv[e]; acc[5] += y1[1] * wv[e];
       acc[6] += y1[2] * wv[e];
@@ -322,9 +327,15 @@ __global__ __launch_bounds__(CW * 64) void composite_fwd_kernel(mli_composite_ar
     }
   }
 #pragma unroll
-  for (int i = 0; i < 12; ++i) acc[i] = wave_sum(acc[i]);
-  if (lane != 0) return;
-  float rgb[3] = {acc[0], acc[1], acc[2]}, orr[3] = {acc[3], acc[4], acc[5]}, os = acc[6];
+  for (int i = 0; i < 12; ++i) acc[i] = __shfl(wave_sum(acc[i]), 0);
+}
+
+// Composited outputs with the white background and o_re (NeuralLumen/model.py:266-305).
+MLI_FI void composite_outputs(const mli_composite_args& a, const float (&acc)[12], float (&rgb)[3], float (&orr)[3],
+                              float& os, float (&ore)[3]) {
+  rgb[0] = acc[0]; rgb[1] = acc[1]; rgb[2] = acc[2];
+  orr[0] = acc[3]; orr[1] = acc[4]; orr[2] = acc[5];
+  os = acc[6];
   const float op = acc[7];
   if (a.white_bg) {
     for (int i = 0; i < 3; ++i) {
@@ -333,16 +344,139 @@ __global__ __launch_bounds__(CW * 64) void composite_fwd_kernel(mli_composite_ar
     }
     os = os + (1.f - op);
   }
+  for (int i = 0; i < 3; ++i) ore[i] = rgb[i] - orr[i] * os;
+}
+
+__global__ __launch_bounds__(CW * 64) void composite_fwd_kernel(mli_composite_args a) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = blockIdx.x * CW + w;
+  if (r >= a.R) return;  // whole wave exits (no block barriers below)
+  float wv[CE], yk[CE][7], acc[12];
+  composite_ray(a, r, lane, wv, yk, acc);
+  if (lane != 0) return;
+  float rgb[3], orr[3], os, ore[3];
+  composite_outputs(a, acc, rgb, orr, os, ore);
   for (int i = 0; i < 3; ++i) {
     a.rgb[3 * r + i] = rgb[i];
     a.o_r[3 * r + i] = orr[i];
-    a.o_re[3 * r + i] = rgb[i] - orr[i] * os;
+    a.o_re[3 * r + i] = ore[i];
   }
   a.o_s[r] = os;
-  if (a.opacity) a.opacity[r] = op;
+  if (a.opacity) a.opacity[r] = acc[7];
   if (a.gradient) for (int i = 0; i < 3; ++i) a.gradient[3 * r + i] = acc[8 + i];
   if (a.depth) a.depth[r] = acc[11] / a.ray_norm[r];
   if (a.blend_dist) a.blend_dist[r] = acc[11];  // render.composite(dists, weights)
+}
+
+// d total / d (rgb, o_r, o_s, o_re) of one ray -> the per-sample pre-sigmoid gradients (scaled)
+// of its samples: the composite + o_re + sigmoid backward (one definition for both paths).
+MLI_FI void composite_bwd_sample(const float (&dr_in)[3], const float (&dor_in)[3], float d_o_s,
+                                 const float (&d_o_re)[3], const float (&orr)[3], float os, float w,
+                                 const float (&y)[7], f32x4& o0, f32x4& o1) {
+  float dr[3], dor[3];
+  float sre = 0.f;
+  for (int i = 0; i < 3; ++i) {
+    const float dre = d_o_re[i];
+    dr[i] = dr_in[i] + dre;
+    dor[i] = dor_in[i] - dre * os;
+    sre += dre * orr[i];
+  }
+  const float dos = d_o_s - sre;
+  o0[0] = w * dr[0] * (y[0] * (1.f - y[0]));
+  o0[1] = w * dr[1] * (y[1] * (1.f - y[1]));
+  o0[2] = w * dr[2] * (y[2] * (1.f - y[2]));
+  o0[3] = w * dor[0] * (y[3] * (1.f - y[3]));
+  o1[0] = w * dor[1] * (y[4] * (1.f - y[4]));
+  o1[1] = w * dor[2] * (y[5] * (1.f - y[5]));
+  o1[2] = w * dos * (y[6] * (1.f - y[6]));
+  o1[3] = 0.f;
+}
+
+// Fused stage-b training tail, one wave per ray: composite (as composite_fwd_kernel), the loss
+// terms and d total / d outputs of the ray (mli_loss::ray_terms, as terms_kernel), its samples'
+// eikonal / curvature terms, and the composite backward of its samples (as composite_bwd_kernel)
+// -- the composited outputs and the loss gradients never leave registers.  Loss values: one
+// partial sum per workgroup and accumulator; composite_loss_finalize adds them up.  (A
+// last-workgroup-done counter in this kernel instead cost 80 us per launch: each workgroup's
+// agent-scope release writes back its XCD's whole L2.)
+__global__ __launch_bounds__(CW * 64) void composite_loss_kernel(mli_composite_loss_args A) {
+  using namespace mli_loss;
+  const mli_composite_args& a = A.comp;
+  const mli_loss_args& L = A.loss;
+  __shared__ float red[4 * CW], mm[4], part[CW][ACC_N];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (L.w_intrinsic != 0.f) block_minmax<CW * 64>(L, red, mm);
+  const int R = a.R, N = a.N;
+  const int r = blockIdx.x * CW + w;
+  float acc[ACC_N];
+#pragma unroll
+  for (int i = 0; i < ACC_N; ++i) acc[i] = 0.f;
+  if (r < R) {
+    float wv[CE], yk[CE][7], cs[12];
+    composite_ray(a, r, lane, wv, yk, cs);
+    float rgb[3], orr[3], os, ore[3];
+    composite_outputs(a, cs, rgb, orr, os, ore);
+    if (lane == 0) {
+      for (int i = 0; i < 3; ++i) {
+        a.rgb[3 * r + i] = rgb[i];
+        a.o_r[3 * r + i] = orr[i];
+        a.o_re[3 * r + i] = ore[i];
+      }
+      a.o_s[r] = os;
+    }
+    // every lane forms the ray's gradients (same inputs, same arithmetic); lane 0 counts its terms
+    float ra[ACC_N] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float d_rgb[3], d_o_r[3], d_o_s, d_o_re[3];
+    ray_terms(L, r, mm, rgb, orr, os, ore, ra, d_rgb, d_o_r, d_o_s, d_o_re);
+    if (lane == 0) {
+      acc[0] = ra[0]; acc[1] = ra[1]; acc[4] = ra[4]; acc[5] = ra[5]; acc[6] = ra[6]; acc[7] = ra[7];
+    }
+    const bool outside = L.outside[r] != 0;
+#pragma unroll
+    for (int e = 0; e < CE; ++e) {
+      const int k = CE * lane + e;
+      if (k < N) {
+        const size_t s = (size_t)k * R + r;
+        if (!outside) sample_terms(L, s, acc);
+        f32x4 o0, o1;
+        composite_bwd_sample(d_rgb, d_o_r, d_o_s, d_o_re, orr, os, wv[e] * A.grad_scale, yk[e], o0, o1);
+        *reinterpret_cast<f32x4*>(A.dz4 + 8 * s) = o0;
+        *reinterpret_cast<f32x4*>(A.dz4 + 8 * s + 4) = o1;
+      }
+    }
+    acc[2] = wave_sum(acc[2]);
+    acc[3] = wave_sum(acc[3]);
+  }
+  if (lane == 0)
+    for (int i = 0; i < ACC_N; ++i) part[w][i] = acc[i];
+  __syncthreads();
+  if (threadIdx.x < ACC_N) {
+    float t = 0.f;
+    for (int v = 0; v < CW; ++v) t += part[v][threadIdx.x];
+    L.scratch[(size_t)blockIdx.x * ACC_N + threadIdx.x] = t;
+  }
+}
+
+// The loss values from the workgroup partials: accumulator i = threadIdx.x / 32; lane j of its 32
+// adds workgroups j, j + 32, ... in order, then a fixed xor tree over the 32 lanes (bit-reproducible).
+__global__ __launch_bounds__(256) void composite_loss_finalize(mli_loss_args L, int nb) {
+  __shared__ float fin[mli_loss::ACC_N];
+  const int i = threadIdx.x >> 5, j = threadIdx.x & 31;
+  float t = 0.f;
+  int b = j;
+  for (; b + 7 * 32 < nb; b += 8 * 32) {  // 8 independent loads in flight, then the adds in order
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = L.scratch[(size_t)(b + 32 * u) * mli_loss::ACC_N + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t += v[u];
+  }
+  for (; b < nb; b += 32) t += L.scratch[(size_t)b * mli_loss::ACC_N + i];
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) t += __shfl_xor(t, o);
+  if (j == 0) fin[i] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) mli_loss::finalize(L, fin);
 }
 
 // Backward of the composite + heads' output sigmoids: one thread per sample (no scan: the
@@ -353,28 +487,19 @@ __global__ __launch_bounds__(256) void composite_bwd_kernel(mli_composite_bwd_ar
   const size_t s = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (s >= S) return;
   const int r = (int)(s % (size_t)R);
-  float dr[3], dor[3];
-  const float os = a.o_s[r];
-  float sre = 0.f;
+  float dr[3], dor[3], dre[3], orr[3];
   for (int i = 0; i < 3; ++i) {
-    const float dre = a.d_o_re ? a.d_o_re[3 * r + i] : 0.f;
-    dr[i] = (a.d_rgb ? a.d_rgb[3 * r + i] : 0.f) + dre;
-    dor[i] = (a.d_o_r ? a.d_o_r[3 * r + i] : 0.f) - dre * os;
-    sre += dre * a.o_r[3 * r + i];
+    dre[i] = a.d_o_re ? a.d_o_re[3 * r + i] : 0.f;
+    dr[i] = a.d_rgb ? a.d_rgb[3 * r + i] : 0.f;
+    dor[i] = a.d_o_r ? a.d_o_r[3 * r + i] : 0.f;
+    orr[i] = a.o_r[3 * r + i];
   }
-  const float dos = (a.d_o_s ? a.d_o_s[r] : 0.f) - sre;
-  const float w = a.weights[s] * a.grad_scale;
+  const float dos = a.d_o_s ? a.d_o_s[r] : 0.f;
   const f32x4 y0 = *reinterpret_cast<const f32x4*>(a.y + 8 * s);
   const f32x4 y1 = *reinterpret_cast<const f32x4*>(a.y + 8 * s + 4);
+  const float y[7] = {y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2]};
   f32x4 o0, o1;
-  o0[0] = w * dr[0] * (y0[0] * (1.f - y0[0]));
-  o0[1] = w * dr[1] * (y0[1] * (1.f - y0[1]));
-  o0[2] = w * dr[2] * (y0[2] * (1.f - y0[2]));
-  o0[3] = w * dor[0] * (y0[3] * (1.f - y0[3]));
-  o1[0] = w * dor[1] * (y1[0] * (1.f - y1[0]));
-  o1[1] = w * dor[2] * (y1[1] * (1.f - y1[1]));
-  o1[2] = w * dos * (y1[2] * (1.f - y1[2]));
-  o1[3] = 0.f;
+  composite_bwd_sample(dr, dor, dos, dre, orr, a.o_s[r], a.weights[s] * a.grad_scale, y, o0, o1);
   *reinterpret_cast<f32x4*>(a.dz4 + 8 * s) = o0;
   *reinterpret_cast<f32x4*>(a.dz4 + 8 * s + 4) = o1;
 }
@@ -604,4 +729,27 @@ extern "C" int mli_ray_batch(const mli_ray_batch_args* a, mli_stream_t s) {
   if (a->n_pixels < a->R || a->n_pixels > (1ll << 40) || !a->ray_idx) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(ray_batch_kernel, dim3((a->R + 255) / 256), dim3(256), 0, (hipStream_t)s, *a);
   MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_composite_loss(const mli_composite_loss_args* a, mli_stream_t s) {
+  const mli_composite_args& c = a->comp;
+  const mli_loss_args& l = a->loss;
+  if (c.R <= 0 || c.N <= 0 || c.N > 256 || l.R != c.R || l.N != c.N) return (int)hipErrorInvalidValue;
+  if (!c.weights || !c.rgb || !c.o_r || !c.o_s || !c.o_re || !a->dz4 || !l.scratch || !l.losses || !l.gt ||
+      !l.outside)
+    return (int)hipErrorInvalidValue;
+  if (l.w_intrinsic != 0.f && (l.sha == nullptr || l.cert == nullptr || l.ref == nullptr))
+    return (int)hipErrorInvalidValue;
+  const int nb = (c.R + CW - 1) / CW;
+  hipLaunchKernelGGL(composite_loss_kernel, dim3(nb), dim3(CW * 64), 0, (hipStream_t)s, *a);
+  hipLaunchKernelGGL(composite_loss_finalize, dim3(1), dim3(256), 0, (hipStream_t)s, l, nb);
+  MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_composite_loss_workspace(const mli_composite_loss_args* a, int64_t* bytes) {
+  const int R = a->comp.R;
+  if (R <= 0 || a->comp.N <= 0) return (int)hipErrorInvalidValue;
+  bytes[0] = (int64_t)mli_loss::ACC_N * ((R + CW - 1) / CW) * 4;  // workgroup partials
+  bytes[1] = (int64_t)R * a->comp.N * 8 * 4;                            // dz4
+  return 0;
 }

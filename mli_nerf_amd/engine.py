@@ -296,16 +296,41 @@ class RenderEngine:
                        depth=torch.empty(R, 1, device=self.device))
             if self.cfg.light_visibility:
                 out["blend_dist"] = torch.empty(R, 1, device=self.device)
-        anneal = min(progress / self.cfg.anneal_end, 1.0)
-        L.call("mli_composite_fwd", L.CompositeArgs(R, N, L.ptr(dists), L.ptr(rays["far"]), L.ptr(rays["ray_unit"]),
-                                                    L.ptr(rays["ray_norm"]), L.ptr(fld["sdf"]), L.ptr(fld["grad"]),
-                                                    L.ptr(hd["y"]), L.ptr(s_var), float(anneal),
-                                                    1 if self.cfg.white_bg else 0, L.ptr(out["weights"]),
-                                                    L.ptr(out["rgb"]), L.ptr(out["o_r"]), L.ptr(out["o_s"]),
-                                                    L.ptr(out["o_re"]), L.ptr(out.get("opacity")),
-                                                    L.ptr(out.get("gradient")), L.ptr(out.get("depth")),
-                                                    L.ptr(out.get("blend_dist"))))
+        L.call("mli_composite_fwd", self._composite_args(rays, dists, fld, hd, s_var, progress, out))
         return out
+
+    def _composite_args(self, rays, dists, fld, hd, s_var, progress, out):
+        N, R = dists.shape
+        anneal = min(progress / self.cfg.anneal_end, 1.0)
+        return L.CompositeArgs(R, N, L.ptr(dists), L.ptr(rays["far"]), L.ptr(rays["ray_unit"]),
+                               L.ptr(rays["ray_norm"]), L.ptr(fld["sdf"]), L.ptr(fld["grad"]), L.ptr(hd["y"]),
+                               L.ptr(s_var), float(anneal), 1 if self.cfg.white_bg else 0, L.ptr(out["weights"]),
+                               L.ptr(out["rgb"]), L.ptr(out["o_r"]), L.ptr(out["o_s"]), L.ptr(out["o_re"]),
+                               L.ptr(out.get("opacity")), L.ptr(out.get("gradient")), L.ptr(out.get("depth")),
+                               L.ptr(out.get("blend_dist")))
+
+    @staticmethod
+    def grad_scale(R):
+        """Power-of-two loss scale of the fp16 backward images (undone in mli_grad_assemble)."""
+        return float(2.0 ** round(math.log2(max(R, 1)) + 2))
+
+    @torch.no_grad()
+    def composite_loss(self, rays, dists, fld, hd, s_var, progress, loss):
+        """Fused training tail (mli_composite_loss): composite + stage-b losses + composite
+        backward in one launch.  ``loss``: an L.LossArgs carrying the loss inputs, weights and the
+        losses[8] output (its rgb / o_r / o_s / o_re / d_* fields are not read).  Returns the
+        composite dict and dz4 for backward()."""
+        N, R = dists.shape
+        out = dict(weights=self._buf("weights", (N, R)),
+                   rgb=torch.empty(R, 3, device=self.device), o_r=torch.empty(R, 3, device=self.device),
+                   o_s=torch.empty(R, 1, device=self.device), o_re=torch.empty(R, 3, device=self.device))
+        dz4 = self._buf("dz4", (N, R, 8))
+        args = L.CompositeLossArgs(self._composite_args(rays, dists, fld, hd, s_var, progress, out), loss,
+                                   self.grad_scale(R), L.ptr(dz4))
+        n = L.workspace("mli_composite_loss", args)[0] // 4
+        args.loss.scratch = L.ptr(self._buf("cl_scratch", (n,)))
+        L.call("mli_composite_loss", args)
+        return out, dz4
 
     @torch.no_grad()
     def light_visibility(self, rays, comp, iters=20):
@@ -351,12 +376,16 @@ class RenderEngine:
                 return
         raise RuntimeError("render state of an unknown engine lane")
 
-    def render(self, data, s_var, progress, training, u=None, W=512):
+    def render(self, data, s_var, progress, training, u=None, W=512, composite=True):
+        """rays -> sampling -> FIELD -> heads -> composite; ``composite=False`` stops after the
+        heads (comp None: the fused training tail, composite_loss, composites)."""
         self._bufs["__gen"] = self._bufs.get("__gen", 0) + 1
         rays = self.rays(data["pose"], data["intr"], data["pose_light"], data["ray_idx"], W)
         dists = self.sample(rays, u)
         fld = self.field(rays, dists, training)
         hd = self.heads(rays, dists, fld, training)
+        if not composite:
+            return rays, dists, fld, hd, None
         comp = self.composite(rays, dists, fld, hd, s_var, progress, training)
         if self.cfg.light_visibility and not training:
             self.light_visibility(rays, comp)
@@ -430,18 +459,21 @@ class RenderEngine:
             L.call("mli_wgrad", L.WgradArgs(S, len(jobs), C.cast(jobs, C.c_void_p), cls, det, L.ptr(ws)))
 
     @torch.no_grad()
-    def backward(self, st, d_rgb, d_o_r, d_o_s, d_o_re, flat, sdf_l1, grad_out):
-        """Gradient of the loss w.r.t. the trainable head parameters into grad_out (flat)."""
+    def backward(self, st, d_rgb, d_o_r, d_o_s, d_o_re, flat, sdf_l1, grad_out, dz4=None):
+        """Gradient of the loss w.r.t. the trainable head parameters into grad_out (flat), from
+        d loss / d (rgb, o_r, o_s, o_re) -- or from ``dz4`` when composite_loss already ran the
+        composite backward (the d_* are then unused)."""
         rays, dists, fld, hd, comp = st
         N, R = dists.shape
         S = N * R
-        scale = float(2.0 ** round(math.log2(max(R, 1)) + 2))
-        dz4 = self._buf("dz4", (N, R, 8))
-        c = lambda t: None if t is None else t.contiguous()  # noqa: E731
-        L.call("mli_composite_bwd", L.CompositeBwdArgs(R, N, L.ptr(comp["weights"]), L.ptr(hd["y"]),
-                                                       L.ptr(comp["o_r"]), L.ptr(comp["o_s"]), L.ptr(c(d_rgb)),
-                                                       L.ptr(c(d_o_r)), L.ptr(c(d_o_s)), L.ptr(c(d_o_re)),
-                                                       scale, L.ptr(dz4)))
+        scale = self.grad_scale(R)
+        if dz4 is None:
+            dz4 = self._buf("dz4", (N, R, 8))
+            c = lambda t: None if t is None else t.contiguous()  # noqa: E731
+            L.call("mli_composite_bwd", L.CompositeBwdArgs(R, N, L.ptr(comp["weights"]), L.ptr(hd["y"]),
+                                                           L.ptr(comp["o_r"]), L.ptr(comp["o_s"]), L.ptr(c(d_rgb)),
+                                                           L.ptr(c(d_o_r)), L.ptr(c(d_o_s)), L.ptr(c(d_o_re)),
+                                                           scale, L.ptr(dz4)))
         dz4T = self._buf("dz4T", (3, 4, S), torch.float16)
         dwbuf = self._buf("dw", (self._dw_total(),))
         if not self.deterministic:

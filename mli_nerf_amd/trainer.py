@@ -150,6 +150,10 @@ def reduce_gradients(grad, world_size, group=None):
 class Trainer:
     """Stage-b / stage-a trainer: ``train_step(data)`` = forward + loss + backward + AdamW."""
 
+    # stage b: composite + losses + composite backward as ONE launch (mli_composite_loss);
+    # False: the three calls mli_composite_fwd / mli_stage_b_loss / mli_composite_bwd
+    fused_tail = True
+
     def __init__(self, cfg, is_inference=True, seed=0, model=None, world_size=None):
         self.cfg = cfg
         self.is_inference = is_inference
@@ -387,24 +391,33 @@ class Trainer:
         m.prepare()
         m.image_width = m.image_size_train[1]
         eng = m.engine
+        fused = self.fused_tail
         if pf is None:
             st = eng.render(data, m.s_var.detach(), m.progress, True, u=m.stratified_uniforms(data, u),
-                            W=m.image_width)
+                            W=m.image_width, **({"composite": False} if fused else {}))
         else:
             lane, rays, dists, fld, done = pf
             torch.cuda.current_stream(m.flat.device).wait_event(done)
             eng.use_lane(lane)
             hd = eng.heads(rays, dists, fld, True)
-            comp = eng.composite(rays, dists, fld, hd, m.s_var.detach(), m.progress, True)
+            comp = None if fused else eng.composite(rays, dists, fld, hd, m.s_var.detach(), m.progress, True)
             st = (rays, dists, fld, hd, comp)
         if self.prefetch_gate == "heads":
             self._gate_ev = torch.cuda.Event()
             self._gate_ev.record()
         eng.gate_wgrad = self.prefetch_gate == "wgrad"
-        m._last_state = st
         grad, lv = self._grad_buffer()  # every element is written by the backward / the loss kernel
-        d_rgb, d_o_r, d_o_s, d_o_re = self._fused_losses(st, data, lv)
-        eng.backward(st, d_rgb, d_o_r, d_o_s, d_o_re, m.flat, m._sdf_l1(), grad)
+        if fused:
+            # composite + losses + composite backward in one launch (mli_composite_loss)
+            rays, dists, fld, hd, _ = st
+            comp, dz4 = eng.composite_loss(rays, dists, fld, hd, m.s_var.detach(), m.progress,
+                                           self._loss_args(rays, fld, None, data, lv))
+            st = (rays, dists, fld, hd, comp)
+            eng.backward(st, None, None, None, None, m.flat, m._sdf_l1(), grad, dz4=dz4)
+        else:
+            d_rgb, d_o_r, d_o_s, d_o_re = self._fused_losses(st, data, lv)
+            eng.backward(st, d_rgb, d_o_r, d_o_s, d_o_re, m.flat, m._sdf_l1(), grad)
+        m._last_state = st
         if eng.gate_wgrad:
             self._gate_ev, eng.gate_event = eng.gate_event, None
         reduce_gradients(self._grad, self.world_size)   # gradients + metrics, one collective
@@ -414,8 +427,29 @@ class Trainer:
         self._publish(lv)
         return m.outputs(st) if return_outputs else None
 
+    def _loss_args(self, rays, fld, comp, data, lv, d=(None, None, None, None), scratch=None):
+        """mli_loss_args of this step: the loss inputs, weights and factors (trainer.py:133-149
+        of the reference), the composited outputs (``comp``; None for mli_composite_loss, which
+        keeps them in registers), the gradient outputs ``d`` and the losses[8] slot ``lv``."""
+        R, N = rays["outside"].shape[0], fld["sdf"].shape[0]
+        w = self.weights
+        intr = "intrinsic" in w
+        cp = (lambda k: None) if comp is None else (lambda k: L.ptr(comp[k]))  # noqa: E731
+        self._keep = [_c(data["image_sampled"])] + [_c(data.get(k)) if intr else None for k in (
+            "pseudo_ref_sampled", "pseudo_sha_sampled", "pseudo_visibility_certainty_sampled")]
+        gt, ref, sha, cert = self._keep
+        return L.LossArgs(
+            R, N, cp("rgb"), cp("o_r"), cp("o_s"), cp("o_re"), L.ptr(gt), L.ptr(ref), L.ptr(sha), L.ptr(cert),
+            L.ptr(rays["outside"]), L.ptr(fld["grad"]) if "eikonal" in w else None,
+            L.ptr(fld["hess"]) if "curvature" in w else None,
+            w.get("render", 0.0), w.get("eikonal", 0.0), w.get("curvature", 0.0), w.get("intrinsic", 0.0),
+            w.get("regularize_re", 0.0), self.ranges[0][0], self.ranges[0][1], self.ranges[1][0],
+            self.ranges[1][1], self.intr_factors[0], self.intr_factors[1], *self.re_factors,
+            *[L.ptr(t) for t in d], L.ptr(lv), L.ptr(scratch))
+
     def _fused_losses(self, st, data, lv):
-        """mli_stage_b_loss: loss values + d total / d (rgb, o_r, o_s, o_re)."""
+        """mli_stage_b_loss: loss values + d total / d (rgb, o_r, o_s, o_re) (the three-call tail,
+        ``fused_tail = False``, and stage a)."""
         m, eng = self.model, self.model.engine
         rays, dists, fld, hd, comp = st
         N, R = dists.shape
@@ -424,19 +458,8 @@ class Trainer:
         n = L.workspace("mli_stage_b_loss", L.LossArgs(R, N))[0] // 4
         if self._scratch is None or self._scratch.device != m.flat.device or self._scratch.numel() < n:
             self._scratch = torch.empty(n, device=m.flat.device)
-        w = self.weights
-        intr = "intrinsic" in w
-        L.call("mli_stage_b_loss", L.LossArgs(
-            R, N, L.ptr(comp["rgb"]), L.ptr(comp["o_r"]), L.ptr(comp["o_s"]), L.ptr(comp["o_re"]),
-            L.ptr(_c(data["image_sampled"])), L.ptr(_c(data.get("pseudo_ref_sampled")) if intr else None),
-            L.ptr(_c(data.get("pseudo_sha_sampled")) if intr else None),
-            L.ptr(_c(data.get("pseudo_visibility_certainty_sampled")) if intr else None),
-            L.ptr(rays["outside"]), L.ptr(fld["grad"]) if "eikonal" in w else None,
-            L.ptr(fld["hess"]) if "curvature" in w else None,
-            w.get("render", 0.0), w.get("eikonal", 0.0), w.get("curvature", 0.0), w.get("intrinsic", 0.0),
-            w.get("regularize_re", 0.0), self.ranges[0][0], self.ranges[0][1], self.ranges[1][0],
-            self.ranges[1][1], self.intr_factors[0], self.intr_factors[1], *self.re_factors,
-            L.ptr(d_rgb), L.ptr(d_o_r), L.ptr(d_o_s), L.ptr(d_o_re), L.ptr(lv), L.ptr(self._scratch)))
+        L.call("mli_stage_b_loss", self._loss_args(rays, fld, comp, data, lv, (d_rgb, d_o_r, d_o_s, d_o_re),
+                                                   self._scratch))
         return d_rgb, d_o_r, d_o_s, d_o_re
 
     def compute_grads_a(self, data, u=None):

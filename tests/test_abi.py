@@ -27,6 +27,7 @@ STRUCTS = {
     "mli_sdf_bwd_args": L.SdfBwdArgs, "mli_pack_sdf_t_args": L.PackSdfTArgs, "mli_hash_bwd_args": L.HashBwdArgs,
     "mli_frag_rows_args": L.FragRowsArgs, "mli_light_visibility_args": L.LightVisibilityArgs,
     "mli_ray_batch_args": L.RayBatchArgs, "mli_heads_bwd_args": L.HeadsBwdArgs,
+    "mli_composite_loss_args": L.CompositeLossArgs,
 }
 
 
@@ -67,10 +68,12 @@ def test_library_exports_header_entry_points():
     assert lib.mli_abi_version() == L.ABI_VERSION
     fns = _declared_functions()
     queries = {n + "_workspace" for n in L.WORKSPACE}
-    assert set(L.ENTRY_POINTS) | {"mli_abi_version", "mli_error_string"} | queries == set(fns)
+    assert set(L.ENTRY_POINTS) | {"mli_abi_version", "mli_error_string", "mli_source_hash"} | queries == set(fns)
     for name in fns:
         assert hasattr(lib, name), name
     assert lib.mli_error_string(0)
+    from mli_nerf_amd import build as B
+    assert lib.mli_source_hash().decode() == B.source_hash() == B.built_hash(L.LIB_PATH)
 
 
 def test_product_path_does_not_import_oracle():

@@ -81,7 +81,8 @@ def test_reference_adamw_matches_fused_trainer():
         total.backward()
         if step == 0:
             assert torch.equal(ma.flat.grad, mb.flat_grad_from_params())
-            assert float(tra.losses["total"]) == float(total)
+            # the fused tail (mli_composite_loss) sums the loss terms in another fixed order
+            assert abs(float(tra.losses["total"]) - float(total.detach())) <= 1e-6 * abs(float(total.detach()))
         opt.step()
         opt.zero_grad(set_to_none=True)
         diff = (ma.flat - mb.flat).abs().max().item()

@@ -368,3 +368,127 @@ def test_prefetch_pipeline_matches_serial_steps(gate):
         print("step", k, "loss", l0, l1, "param max diff", (p0 - p1).abs().max().item())
         assert abs(l0 - l1) <= 1e-6 * max(1.0, abs(l0)), k
         assert (p0 - p1).abs().max().item() <= 1e-6 * p0.abs().max().item(), k
+
+
+@pytest.mark.parametrize("case,R", [("hotdog", 256), ("pikachu", 128), ("render_only", 64)])
+def test_fused_tail_matches_three_calls(case, R):
+    """mli_composite_loss (composite + losses + composite backward in one launch, the default
+    stage-b tail) against mli_composite_fwd / mli_stage_b_loss / mli_composite_bwd on the same
+    render, deterministic mode: composited outputs, weights and the parameter gradient bit-identical
+    (one definition of each formula), loss values 1e-6 relative (the same sums in another fixed
+    order), and two fused steps bit-identical (the partials are summed in a fixed order).
+    'render_only' turns the intrinsic / eikonal / curvature / regularize_re terms off."""
+    _need_gpu()
+    from mli_nerf_amd.trainer import Trainer
+    config = {"pikachu": "NRHints_Pikachu_b"}.get(case, "syn_hotdog_b")
+    Nc = 16
+    model, sd, data, pcfg, (Hh, W) = build(config, R, Nc, 4, 4, 14, 3.0)
+    cfg = preset(config, rays=R, n_coarse=Nc, n_fine=4, log2T=14)
+    cfg.trainer["deterministic"] = True
+    if case == "render_only":
+        for k in list(cfg.trainer.loss_weight):
+            if k != "render":
+                cfg.trainer.loss_weight[k] = 0.0
+    u = torch.rand(1, R, Nc).to(DEV)
+    dd = to_dev(data)
+    tr = Trainer(cfg, is_inference=False, model=model)
+    tr.optim.lr = 0.0
+    tr.optim.wd = 0.0
+    res = {}
+    for fused in (False, True, True):
+        tr.fused_tail = fused
+        tr.current_iteration = 0
+        out = tr.train_step(dd, u=u, return_outputs=True)
+        torch.cuda.synchronize()
+        comp = model._last_state[4]
+        res.setdefault(fused, []).append(dict(
+            losses={k: float(v) for k, v in tr.losses.items()}, psnr=float(tr.metrics["psnr"]),
+            grad=model.flat.grad.detach().clone(),
+            comp={k: comp[k].detach().clone() for k in ("weights", "rgb", "o_r", "o_s", "o_re")},
+            rgb=out["rgb"].detach().clone()))
+    three, f1, f2 = res[False][0], res[True][0], res[True][1]
+    print(case, R, "three", three["losses"], "fused", f1["losses"])
+    for k in three["comp"]:
+        assert torch.equal(three["comp"][k], f1["comp"][k]), k
+    assert torch.equal(three["rgb"], f1["rgb"])
+    for k in three["losses"]:
+        assert abs(three["losses"][k] - f1["losses"][k]) <= 1e-6 * max(1.0, abs(three["losses"][k])), k
+    assert abs(three["psnr"] - f1["psnr"]) < 1e-5
+    assert torch.equal(three["grad"], f1["grad"]), (three["grad"] - f1["grad"]).abs().max().item()
+    assert f1["losses"] == f2["losses"] and torch.equal(f1["grad"], f2["grad"])
+
+
+@pytest.mark.parametrize("R,N,intr", [(151, 37, True), (5, 128, True), (1024, 64, False)])
+def test_composite_loss_kernel_ragged(R, N, intr):
+    """mli_composite_loss against the three calls through the C ABI on random inputs of shapes
+    the trainer never produces: R not a multiple of the 4 rays per workgroup, N not a multiple of
+    the 4 samples per lane, outside rays, NaN-free random sdf / grad / hess / head outputs.
+    Outputs and dz4 bit-identical, loss values 1e-6 relative."""
+    _need_gpu()
+    from mli_nerf_amd import _lib as L
+    g = torch.Generator().manual_seed(R * 1000 + N)
+    rnd = lambda *s: torch.rand(*s, generator=g).to(DEV)  # noqa: E731
+    dists = torch.sort(rnd(R, N) * 2 + 0.5, dim=1).values.t().contiguous()
+    far = dists[-1] + 0.1
+    v = torch.nn.functional.normalize(rnd(R, 3) - 0.5, dim=-1).contiguous()
+    ray_norm = rnd(R) + 0.5
+    sdf = (rnd(N, R) - 0.5) * 0.2
+    grad = (rnd(N, R, 3) - 0.5) * 3
+    hess = (rnd(N, R, 3) - 0.5) * 10
+    y = rnd(N, R, 8)
+    s_var = torch.tensor([3.0], device=DEV)
+    gt, ref, sha, cert = rnd(R, 3), rnd(R, 3), rnd(R), rnd(R)
+    outside = (rnd(R) < 0.2).to(torch.uint8)
+    w = (1.0, 0.1, 5e-4, 1.0 if intr else 0.0, 1.0)
+
+    def comp_bufs():
+        return dict(weights=torch.empty(N, R, device=DEV), rgb=torch.empty(R, 3, device=DEV),
+                    o_r=torch.empty(R, 3, device=DEV), o_s=torch.empty(R, 1, device=DEV),
+                    o_re=torch.empty(R, 3, device=DEV))
+
+    def cargs(o):
+        return L.CompositeArgs(R, N, L.ptr(dists), L.ptr(far), L.ptr(v), L.ptr(ray_norm), L.ptr(sdf), L.ptr(grad),
+                               L.ptr(y), L.ptr(s_var), 0.3, 1, L.ptr(o["weights"]), L.ptr(o["rgb"]), L.ptr(o["o_r"]),
+                               L.ptr(o["o_s"]), L.ptr(o["o_re"]), None, None, None, None)
+
+    def largs(o, d, lv, scratch):
+        cp = (lambda k: None) if o is None else (lambda k: L.ptr(o[k]))  # noqa: E731
+        return L.LossArgs(R, N, cp("rgb"), cp("o_r"), cp("o_s"), cp("o_re"), L.ptr(gt),
+                          L.ptr(ref) if intr else None, L.ptr(sha) if intr else None, L.ptr(cert) if intr else None,
+                          L.ptr(outside), L.ptr(grad), L.ptr(hess), *w, 0.0, 1.0, 0.2, 0.9, 1.0, 1.0, 10.0, 1.0, 1.0,
+                          *[L.ptr(t) for t in d], L.ptr(lv), L.ptr(scratch))
+
+    scale = 2.0 ** 10
+    # three calls
+    o3 = comp_bufs()
+    L.call("mli_composite_fwd", cargs(o3))
+    d = (torch.empty(R, 3, device=DEV), torch.empty(R, 3, device=DEV), torch.empty(R, 1, device=DEV),
+         torch.empty(R, 3, device=DEV))
+    lv3 = torch.empty(8, device=DEV)
+    n3 = L.workspace("mli_stage_b_loss", L.LossArgs(R, N))[0] // 4
+    L.call("mli_stage_b_loss", largs(o3, d, lv3, torch.empty(n3, device=DEV)))
+    dz3 = torch.empty(N, R, 8, device=DEV)
+    L.call("mli_composite_bwd", L.CompositeBwdArgs(R, N, L.ptr(o3["weights"]), L.ptr(y), L.ptr(o3["o_r"]),
+                                                   L.ptr(o3["o_s"]), *[L.ptr(t) for t in d], scale, L.ptr(dz3)))
+    # fused, twice
+    runs = []
+    args = L.CompositeLossArgs(cargs(comp_bufs()), largs(None, (None,) * 4, None, None), scale, None)
+    ws = L.workspace("mli_composite_loss", args)
+    scratch = torch.full((ws[0] // 4,), float("nan"), device=DEV)
+    for _ in range(2):
+        of = comp_bufs()
+        dzf = torch.full((N, R, 8), float("nan"), device=DEV)
+        lvf = torch.empty(8, device=DEV)
+        L.call("mli_composite_loss", L.CompositeLossArgs(cargs(of), largs(None, (None,) * 4, lvf, scratch), scale,
+                                                          L.ptr(dzf)))
+        torch.cuda.synchronize()
+        runs.append((of, dzf, lvf))
+    assert ws[1] == N * R * 8 * 4
+    for of, dzf, lvf in runs:
+        for k in o3:
+            assert torch.equal(o3[k], of[k]), k
+        assert torch.equal(dz3, dzf), (dz3 - dzf).abs().max().item()
+        rel = ((lvf - lv3).abs() / lv3.abs().clamp_min(1.0)).max().item()
+        print(R, N, intr, "losses", lv3.tolist(), "rel", rel)
+        assert rel <= 1e-6
+    assert torch.equal(runs[0][2], runs[1][2])
