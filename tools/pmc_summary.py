@@ -30,6 +30,7 @@ def short(name):
              ("wgrad_kernel<32, 256", "mli_wgrad:thin"), ("encode5_kernel", "mli_sdf:field/encode5"),
              ("field_mlp_kernel", "mli_sdf:field/mlp"), ("sdf_kernel", "mli_sdf:sdf"), ("sample_fine_kernel", "mli_sample_fine"),
              ("composite_fwd_kernel", "mli_composite_fwd"), ("composite_bwd_kernel", "mli_composite_bwd"),
+             ("composite_loss_kernel", "mli_composite_loss"), ("composite_loss_finalize", "mli_composite_loss:finalize"),
              ("adamw_kernel", "mli_adamw"), ("pack_kernel", "mli_pack")]
     for key, val in table:
         if key in name:
