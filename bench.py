@@ -401,12 +401,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MLI_BENCH_REHEARSE=1: rehearse the N-rank path on a one-GPU box -- every rank on cuda:0 and
+    # the collectives on gloo (RCCL refuses two ranks on one device); the line says so
+    rehearse = os.environ.get("MLI_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from mli_nerf_amd import _lib as L, synthetic
     from mli_nerf_amd.configs import preset
@@ -540,6 +548,8 @@ def main():
         "mfma_tflops_step": round(sum(kernel_flops(n, R, N, 64, args.fine, 4, model.stage) for n in ktab) /
                                   (step_ms * 1e-3) / 1e12, 2),
     }
+    if rehearse:  # every rank shared ONE GPU over gloo: a process-flow check, not a scaling number
+        result["config"]["rehearsal"] = "%d ranks on one GPU, gloo collectives" % world
     if stage_a:
         sdf = model.neural_sdf
         result["config"].update(iteration=trainer.current_iteration - 1, active_levels=int(sdf.active_levels),
