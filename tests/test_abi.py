@@ -135,3 +135,24 @@ def test_workspace_queries_match_engine_buffers():
     q.S = 100   # not a multiple of the 64-sample k-step
     with pytest.raises(RuntimeError):
         L.workspace("mli_wgrad", q)
+
+
+def test_source_hash_detects_stale_library(tmp_path, monkeypatch):
+    """build() trusts a library only if the source hash compiled into it (read from the file,
+    not loaded) equals the hash of the in-tree sources + flags; the hash does not depend on the
+    checkout path (the GPU box runs a copy of the tree elsewhere)."""
+    from mli_nerf_amd import build as B
+    if not os.path.exists(L.LIB_PATH):
+        pytest.skip("libmli_hip.so not built")
+    want = B.source_hash()
+    assert B.built_hash(L.LIB_PATH) == want and len(want) == 16
+    fake = tmp_path / "libfake.so"
+    fake.write_bytes(b"\0" * 64 + B.HASH_MARK + b"0123456789abcdef" + b"\0" * 8)
+    assert B.built_hash(str(fake)) == "0123456789abcdef" != want
+    assert B.built_hash(str(tmp_path / "missing.so")) is None
+    # another checkout path, same sources: same hash
+    deps = B._deps()
+    monkeypatch.setattr(B, "_deps", lambda: deps)   # the same files, read from here
+    monkeypatch.setattr(B, "REPO", "/elsewhere/repo")
+    monkeypatch.setattr(B, "FLAGS", [f.replace(ROOT, "/elsewhere/repo") for f in B.FLAGS])
+    assert B.source_hash() == want
