@@ -27,20 +27,23 @@ struct Job {
 struct KArgs {
   Job jobs[MAXJOBS];
   int n_jobs, S, k_split, n_split;
+  int share;                 // SHARE_B layout (see wgrad_kernel): the launch picks that kernel
   float* part;               // deterministic: per-job slabs [n_split][M*K + M], else NULL
   int64_t part_base[MAXJOBS];
 };
 
 // Rows [t*ROWS, t*ROWS + ROWS) x BK samples from k, 8 x 16 B per row, rows clamped to n_rows.
-template <int ROWS, int LOADS>
+template <int ROWS, int LOADS, bool KEEP = false>
 MLI_FI void stage_load(u32x4 (&st)[LOADS], const uint16_t* __restrict__ base, int n_rows, int t,
                        size_t S, int k, int tid) {
 #pragma unroll
   for (int u = 0; u < LOADS; ++u) {
     const int id = u * 512 + tid, row = min(id >> 3, ROWS - 1), col = id & 7;
     const int gr = min(t * ROWS + row, n_rows - 1);
-    // streamed once: non-temporal (leave L2 to the dW atomics)
-    st[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base + gr * S + k + col * 8));
+    const u32x4* src = reinterpret_cast<const u32x4*>(base + gr * S + k + col * 8);
+    // streamed once: non-temporal (leave L2 to the dW atomics); KEEP: rows other workgroups of
+    // this XCD read next (a shared B operand), through L2
+    st[u] = KEEP ? *src : __builtin_nontemporal_load(src);
   }
 }
 
@@ -53,14 +56,23 @@ MLI_FI void stage_store(const u32x4 (&st)[LOADS], uint8_t* lds, int tid) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, int DEPTH>
+template <int BM, int BN, int WM, int WN, int DEPTH, bool SHARE_B = false>
 __global__ __launch_bounds__(512) void wgrad_kernel(KArgs ka) {
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t* la = lds;
   uint8_t* lb = lds + BM * ROWB;
   // locate job / tile / split
-  const int bid = blockIdx.x;
+  int bid = blockIdx.x;
+  if (SHARE_B) {
+    // jobs with one tile each and the same B rows: workgroup b runs on XCD b % 8 (round-robin
+    // dispatch), so the n_jobs jobs of one k-slice take consecutive slots of one XCD and the
+    // slice's B rows come from HBM once, then from that XCD's L2
+    const int xcd = bid & 7, slot = bid >> 3;
+    const int sp = (slot / ka.n_jobs) * 8 + xcd;
+    if (sp >= ka.n_split) return;
+    bid = (slot % ka.n_jobs) * ka.n_split + sp;
+  }
   Job J = ka.jobs[0];
 #pragma unroll
   for (int j = 1; j < MAXJOBS; ++j)
@@ -94,7 +106,7 @@ __global__ __launch_bounds__(512) void wgrad_kernel(KArgs ka) {
   auto load = [&](int d, int kk) MLI_LAMBDA_FI {
     const int kc = min(kk, k1 - BK);
     stage_load<BM, A_LOADS>(sa[d], J.a, J.M, tm, S, kc, tid);
-    stage_load<BN, B_LOADS>(sb[d], J.b, J.K, tn, S, kc, tid);
+    stage_load<BN, B_LOADS, SHARE_B>(sb[d], J.b, J.K, tn, S, kc, tid);
   };
   auto step = [&](int d, int kk) MLI_LAMBDA_FI {
     __syncthreads();
@@ -230,6 +242,11 @@ __global__ __launch_bounds__(512) void frag_rows_kernel(mli_frag_rows_args a) {
 
 enum { CLS_BIG = 1, CLS_WIDE = 2, CLS_THIN = 4 };
 
+#ifndef MLI_WGRAD_WIDE_SHARE
+#define MLI_WGRAD_WIDE_SHARE 1
+#endif
+constexpr bool WIDE_SHARE = MLI_WGRAD_WIDE_SHARE;
+
 inline int job_class(const mli_wgrad_job& j) {
   return j.M <= 32 ? CLS_THIN : (j.K <= 256 ? CLS_BIG : CLS_WIDE);
 }
@@ -238,7 +255,7 @@ inline int job_class(const mli_wgrad_job& j) {
 // grid holds about OCC workgroups per CU (OCC = resident 512-thread workgroups per CU).
 // plan(): the class's jobs and split (host only; also the workspace query); returns the
 // floats of partial slabs the deterministic mode needs, -1 on invalid jobs.
-template <int BM, int BN, int OCC>
+template <int BM, int BN, int OCC, bool SHARE = false>
 int64_t plan(const mli_wgrad_args* a, int cls, KArgs& ka) {
   ka.S = a->S;
   int n = 0, tiles = 0;
@@ -254,7 +271,16 @@ int64_t plan(const mli_wgrad_args* a, int cls, KArgs& ka) {
   ka.n_jobs = n;
   ka.part = nullptr;
   if (n == 0) return 0;
-  const int want = std::max(1, 256 * OCC / tiles);
+  // SHARE: every job is one tile over the same B rows -> the jobs of a k-slice run side by side
+  // on one XCD (wgrad_kernel).  Its 32 CUs must hold them all in one round: a 33rd workgroup on
+  // an XCD doubles the launch (measured 0.44 -> 0.71 ms), so the split is 8 x (32 / jobs).
+  ka.share = 0;
+  if (SHARE) {
+    bool ok = n > 1;
+    for (int i = 0; ok && i < n; ++i) ok = ka.jobs[i].b == ka.jobs[0].b && ka.jobs[i].M <= BM && ka.jobs[i].tiles_n == 1;
+    ka.share = ok ? 1 : 0;
+  }
+  const int want = ka.share ? 8 * std::max(1, 32 * OCC / n) : std::max(1, 256 * OCC / tiles);
   const int steps = a->S / BK;
   ka.k_split = ((steps + want - 1) / want) * BK;
   ka.n_split = (a->S + ka.k_split - 1) / ka.k_split;
@@ -269,10 +295,10 @@ int64_t plan(const mli_wgrad_args* a, int cls, KArgs& ka) {
   return floats;
 }
 
-template <int BM, int BN, int WM, int WN, int OCC, int DEPTH>
+template <int BM, int BN, int WM, int WN, int OCC, int DEPTH, bool SHARE_B = false>
 int launch(const mli_wgrad_args* a, int cls, hipStream_t s) {
   KArgs ka;
-  const int64_t floats = plan<BM, BN, OCC>(a, cls, ka);
+  const int64_t floats = plan<BM, BN, OCC, SHARE_B>(a, cls, ka);
   if (floats < 0) return (int)hipErrorInvalidValue;
   if (ka.n_jobs == 0) return 0;
   if (a->deterministic) {
@@ -281,7 +307,12 @@ int launch(const mli_wgrad_args* a, int cls, hipStream_t s) {
   }
   int grid = 0;
   for (int i = 0; i < ka.n_jobs; ++i) grid += ((ka.jobs[i].M + BM - 1) / BM) * ka.jobs[i].tiles_n * ka.n_split;
-  hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, DEPTH>), dim3(grid), dim3(512), (BM + BN) * ROWB, s, ka);
+  if (SHARE_B && ka.share) {
+    grid = 8 * ka.n_jobs * ((ka.n_split + 7) / 8);
+    hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, DEPTH, true>), dim3(grid), dim3(512), (BM + BN) * ROWB, s, ka);
+  } else {
+    hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, DEPTH>), dim3(grid), dim3(512), (BM + BN) * ROWB, s, ka);
+  }
   if (!a->deterministic) return (int)hipGetLastError();
   RArgs r;
   r.part = a->workspace;
@@ -306,7 +337,7 @@ extern "C" int mli_wgrad(const mli_wgrad_args* a, mli_stream_t s) {
   if (a->S <= 0 || a->S % BK != 0) return (int)hipErrorInvalidValue;
   int e = 0;
   if (a->classes & CLS_BIG) e = launch<256, 256, 4, 2, 1, 2>(a, CLS_BIG, (hipStream_t)s);
-  if (!e && (a->classes & CLS_WIDE)) e = launch<256, 320, 4, 2, 1, 1>(a, CLS_WIDE, (hipStream_t)s);
+  if (!e && (a->classes & CLS_WIDE)) e = launch<256, 320, 4, 2, 1, 1, WIDE_SHARE>(a, CLS_WIDE, (hipStream_t)s);
   if (!e && (a->classes & CLS_THIN)) e = launch<32, 256, 1, 8, 2, 2>(a, CLS_THIN, (hipStream_t)s);
   return e;
 }
@@ -318,7 +349,7 @@ extern "C" int mli_wgrad_workspace(const mli_wgrad_args* a, int64_t* bytes) {
   KArgs ka;
   int64_t mx = 0, f;
   if (a->classes & CLS_BIG) { if ((f = plan<256, 256, 1>(a, CLS_BIG, ka)) < 0) return (int)hipErrorInvalidValue; mx = std::max(mx, f); }
-  if (a->classes & CLS_WIDE) { if ((f = plan<256, 320, 1>(a, CLS_WIDE, ka)) < 0) return (int)hipErrorInvalidValue; mx = std::max(mx, f); }
+  if (a->classes & CLS_WIDE) { if ((f = plan<256, 320, 1, WIDE_SHARE>(a, CLS_WIDE, ka)) < 0) return (int)hipErrorInvalidValue; mx = std::max(mx, f); }
   if (a->classes & CLS_THIN) { if ((f = plan<32, 256, 2>(a, CLS_THIN, ka)) < 0) return (int)hipErrorInvalidValue; mx = std::max(mx, f); }
   bytes[0] = mx * 4;
   return 0;
