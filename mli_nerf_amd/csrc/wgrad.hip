@@ -179,6 +179,144 @@ __global__ __launch_bounds__(512) void wgrad_kernel(KArgs ka) {
   }
 }
 
+// LDS-DMA variant: the operand rows go global -> LDS directly (global_load_lds_dwordx4), NBUF
+// stages of BKD samples in a ring, NBUF - 1 of them in flight while one is consumed -- no
+// register staging, so more bytes in flight per CU than the register-staged kernel can hold
+// (its second stage spills).  A stage is [BM + BN rows][BKD * 2 bytes], unpadded; 16 B chunk c
+// of row r sits at position c ^ ((r >> 2) & 3), so the 16 rows a ds_read_b128 lane group reads
+// cover all 64 banks.  One DMA wave-instruction fills 16 rows (lane l: row l / 4, position l % 4).
+constexpr int BKD = 32;
+constexpr int RBD = BKD * 2;  // bytes per row of a stage
+MLI_FI int swz(int r, int c) { return c ^ ((r >> 2) & 3); }
+
+template <int BM, int BN, int WM, int WN, int NBUF, bool SHARE_B>
+__global__ __launch_bounds__(512) void wgrad_dma_kernel(KArgs ka) {
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  constexpr int ROWS = BM + BN, STAGE = ROWS * RBD;
+  constexpr int PIECES = ROWS / 16, PPW = (PIECES + 7) / 8;  // DMA wave-instructions per stage / wave
+  static_assert(ROWS % 16 == 0, "stage rows");
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  int bid = blockIdx.x;
+  if (SHARE_B) {  // as wgrad_kernel
+    const int xcd = bid & 7, slot = bid >> 3;
+    const int sp = (slot / ka.n_jobs) * 8 + xcd;
+    if (sp >= ka.n_split) return;
+    bid = (slot % ka.n_jobs) * ka.n_split + sp;
+  }
+  Job J = ka.jobs[0];
+#pragma unroll
+  for (int j = 1; j < MAXJOBS; ++j)
+    if (j < ka.n_jobs && bid >= ka.jobs[j].tile_base) J = ka.jobs[j];
+  const int local = bid - J.tile_base;
+  const int split = local % ka.n_split;
+  const int tt = local / ka.n_split;
+  const int tm = tt / J.tiles_n, tn = tt - tm * J.tiles_n;
+  const int k0 = split * ka.k_split;
+  const int k1 = min(ka.S, k0 + ka.k_split);
+  if (k0 >= k1) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave - wm * WN;
+  const int h = lane >> 5, rl = lane & 31;
+  const size_t S = ka.S;
+
+  // this lane's DMA source rows (piece u * 8 + wave, clamped: a duplicate of the last piece
+  // rewrites the same bytes, so every wave issues PPW per stage and the vmcnt counts are uniform)
+  const uint16_t* src[PPW];
+  int dst[PPW];
+#pragma unroll
+  for (int u = 0; u < PPW; ++u) {
+    const int piece = min(u * 8 + wave, PIECES - 1);
+    const int row = piece * 16 + (lane >> 2), pos = lane & 3;
+    const int c = swz(row, pos);  // the chunk that belongs at this position
+    const uint16_t* rp = row < BM ? J.a + (size_t)min(tm * BM + row, J.M - 1) * S
+                                  : J.b + (size_t)min(tn * BN + row - BM, J.K - 1) * S;
+    src[u] = rp + c * 8;
+    dst[u] = piece * 1024;
+  }
+  auto issue = [&](int s, int buf) MLI_LAMBDA_FI {
+    const int kk = min(k0 + s * BKD, k1 - BKD);  // past the end: a dummy refetch, never consumed
+#pragma unroll
+    for (int u = 0; u < PPW; ++u) glds16(src[u] + kk, lds + buf * STAGE + dst[u]);
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  const bool do_bias = (J.db != nullptr) && tn == 0;
+  float bsum = 0.f;  // row (tid >> 1) of the A tile, chunks 2 (tid & 1), 2 (tid & 1) + 1
+
+  const int n_st = (k1 - k0) / BKD;
+#pragma unroll
+  for (int d = 0; d < NBUF - 1; ++d) issue(d, d);
+  for (int st = 0; st < n_st; ++st) {
+    vm_wait((NBUF - 2) * PPW);  // this wave's DMAs of stage st have landed
+    block_sync();               // ... every wave's; and everyone is done with stage st - 1
+    issue(st + NBUF - 1, (st + NBUF - 1) % NBUF);
+    const uint8_t* sb = lds + (st % NBUF) * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < BKD / 16; ++ks) {
+      half8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * TM * 32 + i * 32 + rl;
+        fa[i] = *reinterpret_cast<const half8*>(sb + r * RBD + swz(r, 2 * ks + h) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = BM + wn * TN * 32 + j * 32 + rl;
+        fb[j] = *reinterpret_cast<const half8*>(sb + r * RBD + swz(r, 2 * ks + h) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(fa[i], fb[j], acc[i][j]);
+    }
+    if (do_bias && (tid >> 1) < BM) {
+      const int r = tid >> 1;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const half8 v = *reinterpret_cast<const half8*>(sb + r * RBD + swz(r, 2 * (tid & 1) + u) * 16);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bsum += (float)v[e];
+      }
+    }
+  }
+  vm_wait(0);  // the dummy refetches land before the workgroup's LDS is released
+  float* slab = nullptr;
+  if (ka.part != nullptr) {
+    int jx = 0;
+#pragma unroll
+    for (int j = 1; j < MAXJOBS; ++j)
+      if (j < ka.n_jobs && bid >= ka.jobs[j].tile_base) jx = j;
+    slab = ka.part + ka.part_base[jx] + (int64_t)split * ((int64_t)J.M * J.K + J.M);
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = tm * BM + wm * TM * 32 + i * 32 + acc_row(e, h);
+        const int col = tn * BN + wn * TN * 32 + j * 32 + rl;
+        if (row < J.M && col < J.K) {
+          if (slab) slab[(size_t)row * J.K + col] = acc[i][j][e];
+          else atomicAdd(J.dw + (size_t)row * J.ldw + col, acc[i][j][e]);
+        }
+      }
+  if (do_bias) {
+    bsum += __shfl_xor(bsum, 1);
+    const int row = tm * BM + (tid >> 1);
+    if ((tid & 1) == 0 && (tid >> 1) < BM && row < J.M) {
+      if (slab) slab[(size_t)J.M * J.K + row] = bsum;
+      else atomicAdd(J.db + row, bsum);
+    }
+  }
+}
+
 // Deterministic mode: out = sum over slices 0..n_split-1 (in that order) of the partial slabs.
 // One thread per output element of every job (dW [M][K] then db [M]).
 struct RArgs {
@@ -246,6 +384,11 @@ enum { CLS_BIG = 1, CLS_WIDE = 2, CLS_THIN = 4 };
 #define MLI_WGRAD_WIDE_SHARE 1
 #endif
 constexpr bool WIDE_SHARE = MLI_WGRAD_WIDE_SHARE;
+// WIDE through the LDS-DMA ring (wgrad_dma_kernel) with this many stages; 0: register staging
+#ifndef MLI_WGRAD_WIDE_DMA
+#define MLI_WGRAD_WIDE_DMA 4
+#endif
+constexpr int WIDE_DMA = MLI_WGRAD_WIDE_DMA;
 
 inline int job_class(const mli_wgrad_job& j) {
   return j.M <= 32 ? CLS_THIN : (j.K <= 256 ? CLS_BIG : CLS_WIDE);
@@ -295,7 +438,7 @@ int64_t plan(const mli_wgrad_args* a, int cls, KArgs& ka) {
   return floats;
 }
 
-template <int BM, int BN, int WM, int WN, int OCC, int DEPTH, bool SHARE_B = false>
+template <int BM, int BN, int WM, int WN, int OCC, int DEPTH, bool SHARE_B = false, int DMA_NBUF = 0>
 int launch(const mli_wgrad_args* a, int cls, hipStream_t s) {
   KArgs ka;
   const int64_t floats = plan<BM, BN, OCC, SHARE_B>(a, cls, ka);
@@ -309,7 +452,11 @@ int launch(const mli_wgrad_args* a, int cls, hipStream_t s) {
   for (int i = 0; i < ka.n_jobs; ++i) grid += ((ka.jobs[i].M + BM - 1) / BM) * ka.jobs[i].tiles_n * ka.n_split;
   if (SHARE_B && ka.share) {
     grid = 8 * ka.n_jobs * ((ka.n_split + 7) / 8);
-    hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, DEPTH, true>), dim3(grid), dim3(512), (BM + BN) * ROWB, s, ka);
+    if constexpr (SHARE_B && DMA_NBUF > 0)
+      hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, DMA_NBUF, true>), dim3(grid), dim3(512),
+                         DMA_NBUF * (BM + BN) * RBD, s, ka);
+    else if constexpr (SHARE_B)
+      hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, DEPTH, true>), dim3(grid), dim3(512), (BM + BN) * ROWB, s, ka);
   } else {
     hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, DEPTH>), dim3(grid), dim3(512), (BM + BN) * ROWB, s, ka);
   }
@@ -337,7 +484,7 @@ extern "C" int mli_wgrad(const mli_wgrad_args* a, mli_stream_t s) {
   if (a->S <= 0 || a->S % BK != 0) return (int)hipErrorInvalidValue;
   int e = 0;
   if (a->classes & CLS_BIG) e = launch<256, 256, 4, 2, 1, 2>(a, CLS_BIG, (hipStream_t)s);
-  if (!e && (a->classes & CLS_WIDE)) e = launch<256, 320, 4, 2, 1, 1, WIDE_SHARE>(a, CLS_WIDE, (hipStream_t)s);
+  if (!e && (a->classes & CLS_WIDE)) e = launch<256, 320, 4, 2, 1, 1, WIDE_SHARE, WIDE_DMA>(a, CLS_WIDE, (hipStream_t)s);
   if (!e && (a->classes & CLS_THIN)) e = launch<32, 256, 1, 8, 2, 2>(a, CLS_THIN, (hipStream_t)s);
   return e;
 }
