@@ -1009,9 +1009,15 @@ extern "C" int mli_sdf(const mli_sdf_args* a, mli_stream_t s) {
   }
   if (a->enc == nullptr || a->h0 == nullptr || a->grad == nullptr) return (int)hipErrorInvalidValue;
   // FIELD: phase A (encodings of the 5 points) then phase B (layer 0 + softplus + sdf head),
-  // in chunks of tiles so a chunk's encodings (chunk * 40 KiB) are re-read from the
-  // Infinity Cache instead of HBM
-  constexpr int CHUNK_TILES = 4096;  // 131072 samples, 160 MiB of encodings
+  // in chunks of tiles (a chunk's encodings: tiles x 40 KiB).  Measured at 4096 x 128 samples
+  // with the geometry prefetched beside the heads: 1024 / 2048 / 4096 / 8192 /
+  // 16384 tiles per chunk give FIELD 1.55 / 1.01 / 0.88 / 0.81 / 0.77 ms and steps of 5.49 /
+  // 4.90 / 4.60 / 4.53 / 4.66 ms: each chunk pays a launch tail, and one chunk of 640 MiB
+  // crowds the heads; 8192 (320 MiB, half of it re-read from the Infinity Cache) is kept.
+#ifndef MLI_FIELD_CHUNK_TILES
+#define MLI_FIELD_CHUNK_TILES 8192
+#endif
+  constexpr int CHUNK_TILES = MLI_FIELD_CHUNK_TILES;
   for (int t0 = 0; t0 < tiles; t0 += CHUNK_TILES) {
     const int t1 = t0 + CHUNK_TILES < tiles ? t0 + CHUNK_TILES : tiles;
     hipLaunchKernelGGL(encode5_kernel, dim3((t1 - t0 + 3) / 4), dim3(256), 0, (hipStream_t)s, *a, t0, t1);
