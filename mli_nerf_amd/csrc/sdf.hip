@@ -1022,7 +1022,10 @@ extern "C" int mli_sdf(const mli_sdf_args* a, mli_stream_t s) {
     const int t1 = t0 + CHUNK_TILES < tiles ? t0 + CHUNK_TILES : tiles;
     hipLaunchKernelGGL(encode5_kernel, dim3((t1 - t0 + 3) / 4), dim3(256), 0, (hipStream_t)s, *a, t0, t1);
     int blocks = (t1 - t0 + MLP_WAVES - 1) / MLP_WAVES;
-    if (blocks > 512) blocks = 512;
+#ifndef MLI_FIELD_MLP_BLOCKS
+#define MLI_FIELD_MLP_BLOCKS 512
+#endif
+    if (blocks > MLI_FIELD_MLP_BLOCKS) blocks = MLI_FIELD_MLP_BLOCKS;
     hipLaunchKernelGGL(field_mlp_kernel, dim3(blocks), dim3(MLP_WAVES * 64), LDS_SDF, (hipStream_t)s,
                        *a, t0, t1);
     const int e = (int)hipGetLastError();
