@@ -75,8 +75,11 @@ class RenderEngine:
         self.wsdf = torch.empty(65536 + 5 * 1024 + 16, dtype=torch.uint8, device=self.device)
         self.fplan, fbytes = layout.fwd_plan(self.head_specs)
         self.bplan, bbytes = layout.geo_plan() if stage == "a" else layout.bwd_plan()
-        self.wfwd = torch.empty(fbytes, dtype=torch.uint8, device=self.device)
-        self.wbwd = torch.empty(bbytes, dtype=torch.uint8, device=self.device)
+        # both weight images in one allocation, so one mli_pack call (2 launches) fills them
+        self._bwd_off = (fbytes + 255) // 256 * 256
+        self._wimg = torch.empty(self._bwd_off + bbytes, dtype=torch.uint8, device=self.device)
+        self.wfwd = self._wimg[:fbytes]
+        self.wbwd = self._wimg[self._bwd_off:]
         self.wsdf_t = torch.empty(65536, dtype=torch.uint8, device=self.device) if stage == "a" else None
         self._kmaps = []  # keep host kmap tensors alive
         self.tlayout, self.n_train = layout.trainable_layout(stage)
@@ -130,7 +133,7 @@ class RenderEngine:
         self.load_table(params_flat)
         self.pack_sdf(v0, g0, b0, w_sdf, b_sdf)
 
-    def _descs(self, plan, tensors):
+    def _descs(self, plan, tensors, base=0):
         descs = []
         for p in plan:
             km = torch.from_numpy(p["kmap"].astype(np.int16)).to(self.device)
@@ -141,7 +144,7 @@ class RenderEngine:
             self._kmaps += [km, kmode, nm]
             v, g, b = tensors(p["prefix"])
             descs.append(L.PackLayer(L.ptr(v), L.ptr(g), L.ptr(b), p["n_out"], p["k_ref"], p["transpose"],
-                                     p["n_tiles"], p["k_steps"], L.ptr(km), L.ptr(kmode), p["dst_offset"],
+                                     p["n_tiles"], p["k_steps"], L.ptr(km), L.ptr(kmode), base + p["dst_offset"],
                                      p["chunk_stride"], L.ptr(nm)))
         return descs
 
@@ -156,14 +159,10 @@ class RenderEngine:
         key = (flat.data_ptr(), None if sdf_l1 is None else sdf_l1[0].data_ptr())
         if self._pack_descs is None or self._pack_descs[0] != key:
             self._kmaps = []
-            fd = _to_device_structs(self._descs(self.fplan, tensors), self.device)
-            bd = _to_device_structs(self._descs(self.bplan, tensors), self.device)
-            self._pack_descs = (key, fd, bd, len(self.fplan), len(self.bplan))
-        _, fd, bd, nf, nb = self._pack_descs
-        sf = self._buf("pack_scale_f", (nf, 256))
-        sb = self._buf("pack_scale_b", (nb, 256))
-        L.call("mli_pack", L.PackArgs(nf, L.ptr(fd), L.ptr(self.wfwd), L.ptr(sf)))
-        L.call("mli_pack", L.PackArgs(nb, L.ptr(bd), L.ptr(self.wbwd), L.ptr(sb)))
+            descs = self._descs(self.fplan, tensors) + self._descs(self.bplan, tensors, self._bwd_off)
+            self._pack_descs = (key, _to_device_structs(descs, self.device), len(descs))
+        _, d, n = self._pack_descs
+        L.call("mli_pack", L.PackArgs(n, L.ptr(d), L.ptr(self._wimg), L.ptr(self._buf("pack_scale", (n, 256)))))
 
     def param_view(self, flat, name):
         off, shape = self.toff[name]
