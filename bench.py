@@ -519,7 +519,7 @@ def main():
         # with the prefetch on, an event pair on one stream also times the other stream's
         # kernels: the per-kernel table comes from extra (untimed) steps with the pipeline off
         trainer.train_step(cur)          # retire the prefetched batch
-        k_steps = min(args.steps, 50)
+        k_steps = 200  # >= 1 s of GPU work whatever --steps is (per-kernel averages; a busy GPU for samplers)
         L.PROFILE, L.PROFILE_NAMES = [], names
         for _ in range(k_steps):
             trainer.train_step(next_batch())
