@@ -266,9 +266,33 @@ __global__ __launch_bounds__(FW * 64) void sample_fine_kernel(FineArgs fa) {
 constexpr int CW = 4;  // rays per block
 constexpr int CE = 4;  // samples per lane
 
-// The ray's NeuS alphas, weights (stored) and the wave-reduced composited sums acc[12]
-// (rgb 3, o_r 3, o_s, opacity, gradient 3, sum w d), every lane holding lane 0's values.
+// Scans / sums over the L lanes of one ray (L = 64: the whole wave; L = 32: two rays per wave).
+// For a ray of N <= 32 * CE samples the L = 32 forms give bit-identical results to L = 64: the
+// lanes 32..63 of a 64-lane ray hold the identities (1 for the product, 0 for the sums), and
+// every step the lanes below 32 take is the same in both.
+template <int L>
+MLI_FI float seg_excl_prod(float x, int sub) {
+  float v = x;
+#pragma unroll
+  for (int o = 1; o < L; o <<= 1) {
+    const float y = __shfl_up(v, o, L);
+    if (sub >= o) v *= y;
+  }
+  const float e = __shfl_up(v, 1, L);
+  return sub == 0 ? 1.0f : e;
+}
+template <int L>
+MLI_FI float seg_sum0(float x) {  // the segment's sum as its lane 0 forms it, in every lane
+#pragma unroll
+  for (int o = L / 2; o > 0; o >>= 1) x += __shfl_xor(x, o, L);
+  return __shfl(x, 0, L);
+}
+
+// The ray's NeuS alphas, weights (stored) and the reduced composited sums acc[12] (rgb 3, o_r 3,
+// o_s, opacity, gradient 3, sum w d), every lane of the ray holding its lane 0's values; the ray
+// owns L lanes, lane `sub` of them samples CE*sub .. CE*sub + CE-1.
 // yk: the head outputs each lane read for its samples (kept for the fused backward).
+template <int L>
 MLI_FI void composite_ray(const mli_composite_args& a, int r, int lane, float (&wv)[CE], float (&yk)[CE][7],
                           float (&acc)[12]) {
   const int R = a.R, N = a.N;
@@ -301,7 +325,7 @@ MLI_FI void composite_ray(const mli_composite_args& a, int r, int lane, float (&
     }
     lp *= 1.0f - al[e];
   }
-  float T = wave_excl_prod(lp, lane);
+  float T = seg_excl_prod<L>(lp, lane);
 #pragma unroll
   for (int i = 0; i < 12; ++i) acc[i] = 0.f;
 #pragma unroll
@@ -327,7 +351,7 @@ MLI_FI void composite_ray(const mli_composite_args& a, int r, int lane, float (&
     }
   }
 #pragma unroll
-  for (int i = 0; i < 12; ++i) acc[i] = __shfl(wave_sum(acc[i]), 0);
+  for (int i = 0; i < 12; ++i) acc[i] = seg_sum0<L>(acc[i]);
 }
 
 // Composited outputs with the white background and o_re (NeuralLumen/model.py:266-305).
@@ -347,13 +371,16 @@ MLI_FI void composite_outputs(const mli_composite_args& a, const float (&acc)[12
   for (int i = 0; i < 3; ++i) ore[i] = rgb[i] - orr[i] * os;
 }
 
+// L lanes per ray: 64 / L rays per wave, CW waves per block
+template <int L>
 __global__ __launch_bounds__(CW * 64) void composite_fwd_kernel(mli_composite_args a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int r = blockIdx.x * CW + w;
-  if (r >= a.R) return;  // whole wave exits (no block barriers below)
+  const int sub = lane % L;
+  const int r = (blockIdx.x * CW + w) * (64 / L) + lane / L;
+  if (r >= a.R) return;  // the ray's lanes exit together (no block barriers below)
   float wv[CE], yk[CE][7], acc[12];
-  composite_ray(a, r, lane, wv, yk, acc);
-  if (lane != 0) return;
+  composite_ray<L>(a, r, sub, wv, yk, acc);
+  if (sub != 0) return;
   float rgb[3], orr[3], os, ore[3];
   composite_outputs(a, acc, rgb, orr, os, ore);
   for (int i = 0; i < 3; ++i) {
@@ -399,6 +426,7 @@ MLI_FI void composite_bwd_sample(const float (&dr_in)[3], const float (&dor_in)[
 // partial sum per workgroup and accumulator; composite_loss_finalize adds them up.  (A
 // last-workgroup-done counter in this kernel instead cost 80 us per launch: each workgroup's
 // agent-scope release writes back its XCD's whole L2.)
+template <int LN>
 __global__ __launch_bounds__(CW * 64) void composite_loss_kernel(mli_composite_loss_args A) {
   using namespace mli_loss;
   const mli_composite_args& a = A.comp;
@@ -407,16 +435,17 @@ __global__ __launch_bounds__(CW * 64) void composite_loss_kernel(mli_composite_l
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (L.w_intrinsic != 0.f) block_minmax<CW * 64>(L, red, mm);
   const int R = a.R, N = a.N;
-  const int r = blockIdx.x * CW + w;
+  const int sub = lane % LN;
+  const int r = (blockIdx.x * CW + w) * (64 / LN) + lane / LN;
   float acc[ACC_N];
 #pragma unroll
   for (int i = 0; i < ACC_N; ++i) acc[i] = 0.f;
   if (r < R) {
     float wv[CE], yk[CE][7], cs[12];
-    composite_ray(a, r, lane, wv, yk, cs);
+    composite_ray<LN>(a, r, sub, wv, yk, cs);
     float rgb[3], orr[3], os, ore[3];
     composite_outputs(a, cs, rgb, orr, os, ore);
-    if (lane == 0) {
+    if (sub == 0) {
       for (int i = 0; i < 3; ++i) {
         a.rgb[3 * r + i] = rgb[i];
         a.o_r[3 * r + i] = orr[i];
@@ -428,13 +457,13 @@ __global__ __launch_bounds__(CW * 64) void composite_loss_kernel(mli_composite_l
     float ra[ACC_N] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float d_rgb[3], d_o_r[3], d_o_s, d_o_re[3];
     ray_terms(L, r, mm, rgb, orr, os, ore, ra, d_rgb, d_o_r, d_o_s, d_o_re);
-    if (lane == 0) {
+    if (sub == 0) {
       acc[0] = ra[0]; acc[1] = ra[1]; acc[4] = ra[4]; acc[5] = ra[5]; acc[6] = ra[6]; acc[7] = ra[7];
     }
     const bool outside = L.outside[r] != 0;
 #pragma unroll
     for (int e = 0; e < CE; ++e) {
-      const int k = CE * lane + e;
+      const int k = CE * sub + e;
       if (k < N) {
         const size_t s = (size_t)k * R + r;
         if (!outside) sample_terms(L, s, acc);
@@ -444,9 +473,9 @@ __global__ __launch_bounds__(CW * 64) void composite_loss_kernel(mli_composite_l
         *reinterpret_cast<f32x4*>(A.dz4 + 8 * s + 4) = o1;
       }
     }
-    acc[2] = wave_sum(acc[2]);
-    acc[3] = wave_sum(acc[3]);
   }
+#pragma unroll
+  for (int i = 0; i < ACC_N; ++i) acc[i] = wave_sum(acc[i]);  // the wave's rays and samples
   if (lane == 0)
     for (int i = 0; i < ACC_N; ++i) part[w][i] = acc[i];
   __syncthreads();
@@ -694,7 +723,11 @@ extern "C" int mli_sample_fine(const mli_sample_fine_args* a, mli_stream_t s) {
 extern "C" int mli_composite_fwd(const mli_composite_args* a, mli_stream_t s) {
   if (a->R <= 0) return 0;
   if (a->N > 256) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(composite_fwd_kernel, dim3((a->R + CW - 1) / CW), dim3(CW * 64), 0, (hipStream_t)s, *a);
+  if (a->N <= 32 * CE)  // two rays per wave (bit-identical to one, see seg_excl_prod)
+    hipLaunchKernelGGL(composite_fwd_kernel<32>, dim3((a->R + 2 * CW - 1) / (2 * CW)), dim3(CW * 64), 0,
+                       (hipStream_t)s, *a);
+  else
+    hipLaunchKernelGGL(composite_fwd_kernel<64>, dim3((a->R + CW - 1) / CW), dim3(CW * 64), 0, (hipStream_t)s, *a);
   MLI_LAUNCH_CHECK();
 }
 
@@ -740,8 +773,12 @@ extern "C" int mli_composite_loss(const mli_composite_loss_args* a, mli_stream_t
     return (int)hipErrorInvalidValue;
   if (l.w_intrinsic != 0.f && (l.sha == nullptr || l.cert == nullptr || l.ref == nullptr))
     return (int)hipErrorInvalidValue;
-  const int nb = (c.R + CW - 1) / CW;
-  hipLaunchKernelGGL(composite_loss_kernel, dim3(nb), dim3(CW * 64), 0, (hipStream_t)s, *a);
+  const int rpb = c.N <= 32 * CE ? 2 * CW : CW;  // rays per block: two per wave for N <= 128
+  const int nb = (c.R + rpb - 1) / rpb;
+  if (rpb == 2 * CW)
+    hipLaunchKernelGGL(composite_loss_kernel<32>, dim3(nb), dim3(CW * 64), 0, (hipStream_t)s, *a);
+  else
+    hipLaunchKernelGGL(composite_loss_kernel<64>, dim3(nb), dim3(CW * 64), 0, (hipStream_t)s, *a);
   hipLaunchKernelGGL(composite_loss_finalize, dim3(1), dim3(256), 0, (hipStream_t)s, l, nb);
   MLI_LAUNCH_CHECK();
 }
@@ -749,7 +786,8 @@ extern "C" int mli_composite_loss(const mli_composite_loss_args* a, mli_stream_t
 extern "C" int mli_composite_loss_workspace(const mli_composite_loss_args* a, int64_t* bytes) {
   const int R = a->comp.R;
   if (R <= 0 || a->comp.N <= 0) return (int)hipErrorInvalidValue;
-  bytes[0] = (int64_t)mli_loss::ACC_N * ((R + CW - 1) / CW) * 4;  // workgroup partials
+  const int rpb = a->comp.N <= 32 * CE ? 2 * CW : CW;
+  bytes[0] = (int64_t)mli_loss::ACC_N * ((R + rpb - 1) / rpb) * 4;  // workgroup partials
   bytes[1] = (int64_t)R * a->comp.N * 8 * 4;                            // dz4
   return 0;
 }
