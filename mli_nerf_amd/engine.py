@@ -273,6 +273,12 @@ class RenderEngine:
             y.zero_()  # o_r / o_s slots the single head does not write (composite reads them)
         feat = self._buf("feat", (S * 256,), torch.float16)
         x0T = xT = masks = None
+        if training and self.stage == "b" and not self.deterministic:
+            # the split-K dW accumulators of this lane's backward, zeroed here at the start of the
+            # step, where the GPU is not shared with the prefetched geometry (before the heads
+            # backward the fill competed with the sampling rounds: 5 -> 19 us)
+            self._buf("dw", (self._dw_total(),)).zero_()
+            self._bufs["dw_clean"] = True
         if training:
             x0T = self._buf("x0T", (layout.K0, S), torch.float16)
             xT = self._buf("xT", (nh, 4, 256, S), torch.float16)
@@ -475,8 +481,8 @@ class RenderEngine:
                                                            scale, L.ptr(dz4)))
         dz4T = self._buf("dz4T", (3, 4, S), torch.float16)
         dwbuf = self._buf("dw", (self._dw_total(),))
-        if not self.deterministic:
-            dwbuf.zero_()  # split-K partials add into it (fp32 atomics)
+        if not self.deterministic and not self._bufs.pop("dw_clean", False):
+            dwbuf.zero_()  # split-K partials add into it (fp32 atomics); heads() zeroes it once per render
         if self.heads_bwd == "fused":
             # dX chain + dW of the 256x256 layers in one launch; it writes dZ_0 and dz4 rows for
             # the layer-0 (WIDE) and layer-4 (THIN) dW
