@@ -44,7 +44,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mli_stream_t; /* == hipStream_t */
 
-#define MLI_ABI_VERSION 10
+#define MLI_ABI_VERSION 11
 #define MLI_HIDDEN 256
 #define MLI_LEVELS 16
 #define MLI_LEVEL_FEAT 8
@@ -508,8 +508,13 @@ typedef struct {
                               scratch = workspace bytes[0] (no zeroing needed)                  */
   float grad_scale;        /* as mli_composite_bwd_args */
   float* dz4;              /* [N][R][8], as mli_composite_bwd_args */
+  int defer_finalize;      /* 1: leave the loss values to mli_composite_loss_finalize (the
+                              gradients do not need them; the host issues it where the GPU is
+                              idle, e.g. after the weight gradients)                           */
 } mli_composite_loss_args;
 int mli_composite_loss(const mli_composite_loss_args* a, mli_stream_t s);
+/* The loss values of a deferred mli_composite_loss (same args, same scratch). */
+int mli_composite_loss_finalize(const mli_composite_loss_args* a, mli_stream_t s);
 /* bytes[0]: scratch (workgroup partials); bytes[1]: dz4. */
 int mli_composite_loss_workspace(const mli_composite_loss_args* a, int64_t* bytes);
 

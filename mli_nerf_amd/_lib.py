@@ -99,7 +99,8 @@ class LossArgs(C.Structure):
 
 
 class CompositeLossArgs(C.Structure):
-    _fields_ = [("comp", CompositeArgs), ("loss", LossArgs), ("grad_scale", F32), ("dz4", P)]
+    _fields_ = [("comp", CompositeArgs), ("loss", LossArgs), ("grad_scale", F32), ("dz4", P),
+                ("defer_finalize", I32)]
 
 class PackLayer(C.Structure):
     _fields_ = [("v", P), ("g", P), ("bias", P), ("n_out", I32), ("k_ref", I32), ("transpose", I32),
@@ -184,7 +185,7 @@ class FragRowsArgs(C.Structure):
                 ("ld", I64), ("col0", I64), ("row0", I32)]
 
 
-ABI_VERSION = 10  # include/mli_hip.h MLI_ABI_VERSION
+ABI_VERSION = 11  # include/mli_hip.h MLI_ABI_VERSION
 
 ENTRY_POINTS = {
     "mli_rays": RaysArgs, "mli_hashgrid_fwd": HashgridArgs, "mli_sdf": SdfArgs,
@@ -197,7 +198,7 @@ ENTRY_POINTS = {
     "mli_composite_bwd_geo": CompositeBwdGeoArgs, "mli_geo_bwd": GeoBwdArgs, "mli_sdf_bwd": SdfBwdArgs,
     "mli_pack_sdf_t": PackSdfTArgs, "mli_hash_bwd": HashBwdArgs, "mli_frag_rows": FragRowsArgs,
     "mli_light_visibility": LightVisibilityArgs, "mli_ray_batch": RayBatchArgs,
-    "mli_composite_loss": CompositeLossArgs,
+    "mli_composite_loss": CompositeLossArgs, "mli_composite_loss_finalize": CompositeLossArgs,
 }
 
 # host-only scratch-size queries: int mli_<op>_workspace(const args*, int64_t* bytes) -> how many

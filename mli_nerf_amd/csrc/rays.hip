@@ -779,7 +779,15 @@ extern "C" int mli_composite_loss(const mli_composite_loss_args* a, mli_stream_t
     hipLaunchKernelGGL(composite_loss_kernel<32>, dim3(nb), dim3(CW * 64), 0, (hipStream_t)s, *a);
   else
     hipLaunchKernelGGL(composite_loss_kernel<64>, dim3(nb), dim3(CW * 64), 0, (hipStream_t)s, *a);
-  hipLaunchKernelGGL(composite_loss_finalize, dim3(1), dim3(256), 0, (hipStream_t)s, l, nb);
+  if (!a->defer_finalize) hipLaunchKernelGGL(composite_loss_finalize, dim3(1), dim3(256), 0, (hipStream_t)s, l, nb);
+  MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_composite_loss_finalize(const mli_composite_loss_args* a, mli_stream_t s) {
+  const mli_composite_args& c = a->comp;
+  if (c.R <= 0 || c.N <= 0 || !a->loss.scratch || !a->loss.losses) return (int)hipErrorInvalidValue;
+  const int rpb = c.N <= 32 * CE ? 2 * CW : CW;
+  hipLaunchKernelGGL(composite_loss_finalize, dim3(1), dim3(256), 0, (hipStream_t)s, a->loss, (c.R + rpb - 1) / rpb);
   MLI_LAUNCH_CHECK();
 }
 

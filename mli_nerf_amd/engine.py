@@ -320,7 +320,7 @@ class RenderEngine:
         return float(2.0 ** round(math.log2(max(R, 1)) + 2))
 
     @torch.no_grad()
-    def composite_loss(self, rays, dists, fld, hd, s_var, progress, loss):
+    def composite_loss(self, rays, dists, fld, hd, s_var, progress, loss, defer=False):
         """Fused training tail (mli_composite_loss): composite + stage-b losses + composite
         backward in one launch.  ``loss``: an L.LossArgs carrying the loss inputs, weights and the
         losses[8] output (its rgb / o_r / o_s / o_re / d_* fields are not read).  Returns the
@@ -331,11 +331,19 @@ class RenderEngine:
                    o_s=torch.empty(R, 1, device=self.device), o_re=torch.empty(R, 3, device=self.device))
         dz4 = self._buf("dz4", (N, R, 8))
         args = L.CompositeLossArgs(self._composite_args(rays, dists, fld, hd, s_var, progress, out), loss,
-                                   self.grad_scale(R), L.ptr(dz4))
+                                   self.grad_scale(R), L.ptr(dz4), 1 if defer else 0)
         n = L.workspace("mli_composite_loss", args)[0] // 4
         args.loss.scratch = L.ptr(self._buf("cl_scratch", (n,)))
         L.call("mli_composite_loss", args)
+        if defer:  # the loss values: finish_losses(), once the gradients are issued
+            self._bufs["cl_deferred"] = args
         return out, dz4
+
+    def finish_losses(self):
+        """The loss values of a deferred composite_loss on this lane (mli_composite_loss_finalize)."""
+        args = self._bufs.pop("cl_deferred", None)
+        if args is not None:
+            L.call("mli_composite_loss_finalize", args)
 
     @torch.no_grad()
     def light_visibility(self, rays, comp, iters=20):

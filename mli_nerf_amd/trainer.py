@@ -410,10 +410,13 @@ class Trainer:
         if fused:
             # composite + losses + composite backward in one launch (mli_composite_loss)
             rays, dists, fld, hd, _ = st
+            # (the loss values only after the backward is issued: the finalize then runs at the
+            # step's tail, where the prefetch stream is idle, not beside the sampling rounds)
             comp, dz4 = eng.composite_loss(rays, dists, fld, hd, m.s_var.detach(), m.progress,
-                                           self._loss_args(rays, fld, None, data, lv))
+                                           self._loss_args(rays, fld, None, data, lv), defer=True)
             st = (rays, dists, fld, hd, comp)
             eng.backward(st, None, None, None, None, m.flat, m._sdf_l1(), grad, dz4=dz4)
+            eng.finish_losses()
         else:
             d_rgb, d_o_r, d_o_s, d_o_re = self._fused_losses(st, data, lv)
             eng.backward(st, d_rgb, d_o_r, d_o_s, d_o_re, m.flat, m._sdf_l1(), grad)

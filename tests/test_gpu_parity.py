@@ -492,3 +492,12 @@ def test_composite_loss_kernel_ragged(R, N, intr):
         print(R, N, intr, "losses", lv3.tolist(), "rel", rel)
         assert rel <= 1e-6
     assert torch.equal(runs[0][2], runs[1][2])
+    # deferred loss values (defer_finalize + mli_composite_loss_finalize): the same values
+    of, dzf, lvf = comp_bufs(), torch.empty(N, R, 8, device=DEV), torch.full((8,), float("nan"), device=DEV)
+    da = L.CompositeLossArgs(cargs(of), largs(None, (None,) * 4, lvf, scratch), scale, L.ptr(dzf), 1)
+    L.call("mli_composite_loss", da)
+    torch.cuda.synchronize()
+    assert torch.isnan(lvf).all() and torch.equal(dzf, dz3)   # values not written yet
+    L.call("mli_composite_loss_finalize", da)
+    torch.cuda.synchronize()
+    assert torch.equal(lvf, runs[0][2])
