@@ -64,9 +64,9 @@ def kernel_flops(name, R, N, Nc, Nf, H, stage="b"):
         return 0
     if name == "mli_rgb_bwd":
         return 2 * S * sum(HIDDEN * o + 3 * HIDDEN * HIDDEN for o in HEAD_OUT)
-    if name == "mli_heads_bwd":    # algorithmic: the dX chain (as mli_rgb_bwd) + dW of the 256x256
-        # layers (as mli_wgrad BIG); the W3^T layer its layer-2 workgroups recompute is not counted
-        return kernel_flops("mli_rgb_bwd", R, N, Nc, Nf, H) + kernel_flops("mli_wgrad:big", R, N, Nc, Nf, H)
+    if name == "mli_dw4":          # algorithmic: the output layers' dW (3 / 3 / 1 rows), contracted
+        # in the heads forward (q4) and finished here -- the FLOPs of the THIN class it replaces
+        return 2 * S * HIDDEN * sum(HEAD_OUT)
     if name == "mli_wgrad":
         return 2 * S * heads_fwd
     if name == "mli_wgrad:big":    # dW of the 256x256 hidden layers L1..L3 of the 3 heads
@@ -377,11 +377,10 @@ def main():
     ap.add_argument("--tail", choices=("fused", "three"), default="fused",
                     help="stage-b training tail: fused (mli_composite_loss, one launch) or the three calls "
                          "mli_composite_fwd / mli_stage_b_loss / mli_composite_bwd")
-    ap.add_argument("--heads-bwd", choices=("fused", "split"), default="split",
-                    help="stage-b heads backward: fused (mli_heads_bwd: dX chain + 256x256 dW in one launch) "
-                         "or split (mli_rgb_bwd + mli_wgrad BIG)")
-    ap.add_argument("--heads-split", default="0,0,0",
-                    help="mli_heads_bwd workgroups per (head, layer 1..3), 0 = library default")
+    ap.add_argument("--pq", choices=("on", "off"), default="on",
+                    help="stage-b output-layer dW: on = per-tile partials formed in the heads forward "
+                         "(mli_rgb_fwd PQ mode + mli_dw4; X3 never written), off = X3 through HBM and the "
+                         "THIN split-K class")
     ap.add_argument("--mode", choices=("train", "infer"), default="train",
                     help="train: BASELINE configs[1] step; infer: configs[4] full-frame render")
     ap.add_argument("--frames", type=int, default=4, help="infer: frames timed (after --warmup frames)")
@@ -430,8 +429,7 @@ def main():
     model = model.to(dev)
     trainer = Trainer(cfg, is_inference=False, model=model, world_size=world)
     trainer.fused_tail = args.tail == "fused"
-    model.heads_bwd = args.heads_bwd
-    model.heads_split = tuple(int(x) for x in args.heads_split.split(","))
+    model.pq = args.pq == "on"
     if stage_a:
         # steady state of stage a: past the coarse-to-fine ramp (all 16 levels active)
         trainer.current_iteration = args.iteration
@@ -494,7 +492,7 @@ def main():
     progress("warm-up done (%d steps)" % args.warmup)
     barrier()
     torch.cuda.synchronize()
-    names = None if args.time_all_kernels else {"mli_rgb_fwd", "mli_rgb_bwd", "mli_heads_bwd", "mli_wgrad", "mli_sdf"}
+    names = None if args.time_all_kernels else {"mli_rgb_fwd", "mli_rgb_bwd", "mli_dw4", "mli_wgrad", "mli_sdf"}
     if not args.no_kernel_timing and not pipe:
         L.PROFILE = []  # per-kernel HIP events on the launch stream, over the timed region
         L.PROFILE_NAMES = names
@@ -540,7 +538,8 @@ def main():
         "config": {"workload": "%s stage-%s train step" % (args.config, model.stage), "rays_per_gpu": R,
                    "samples_per_ray": N, "global_rays": R * world, "image": [Hh, W], "parallelism": "dp%d" % world,
                    "pipeline": ("geometry prefetch on a side stream, gate " + args.pipeline) if pipe else "off",
-                   "heads_bwd": args.heads_bwd, "tail": args.tail},
+                   "output_layer_dw": "forward partials (pq)" if args.pq == "on" else "THIN split-K",
+                   "tail": args.tail},
         "kernel_timing": ("HIP events on the launch stream over %d extra steps with the prefetch off" % k_steps)
         if pipe else "HIP events on the launch stream over the timed steps",
         "psnr": round(psnr, 4), "loss": round(loss, 6),

@@ -44,7 +44,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mli_stream_t; /* == hipStream_t */
 
-#define MLI_ABI_VERSION 11
+#define MLI_ABI_VERSION 12
 #define MLI_HIDDEN 256
 #define MLI_LEVELS 16
 #define MLI_LEVEL_FEAT 8
@@ -179,10 +179,24 @@ typedef struct {
   uint16_t* xT;           /* [3 heads][4 layers][256][S] feature-major X1..X4               */
   uint32_t* masks;        /* [3][4][S/32][64][4] ReLU bit masks of X1..X4                   */
   int n_heads;            /* 3: LumenRGB 'rgb_r_s' (stage b); 1: mode 'rgb' (stage a, head mlp) */
+  /* Output-layer partials (training, N % 32 == 0; both NULL: off).  The composite weights do not
+   * depend on the heads, so d loss / d z4[c,s] = D[r,c] * w_s * y_sc (1 - y_sc) with the per-ray
+   * D of mli_composite_loss / mli_composite_bwd (`dray`); the forward reduces, per 256-sample
+   * workgroup wg and ray segment seg (ray floor(256 wg / N) + seg),
+   * q4[wg][seg][head][f][c] = sum_{s of the ray in wg} MLI_Q4_SCALE * w_s y_sc (1 - y_sc) * X3[f,s]
+   * (f < 256; row 256: the sums without X3) while X3 is in registers, and mli_dw4 contracts it
+   * with D.  X3 (the output layer's input) is then not written: xT holds X1..X3 = 3 layers per
+   * head.  Segments past the workgroup's last ray are not written. */
+  const float* weights;   /* [N][R] composite weights of this render (mli_composite_fwd, y = NULL) */
+  float* q4;              /* [S/256][MLI_Q4_SEGS(N)][n_heads][257][4] fp32 */
 } mli_rgb_fwd_args;
+#define MLI_Q4_SCALE 65536.0f
+/* ray segments per 256-sample workgroup (an upper bound; N % 32 == 0) */
+#define MLI_Q4_SEGS(N) ((256 % (N)) == 0 ? 256 / (N) : ((N) % 256 == 0 ? 1 : 256 / (N) + 2))
 int mli_rgb_fwd(const mli_rgb_fwd_args* a, mli_stream_t s);
-/* bytes[0..4]: y, feat_frag, x0T, xT, masks (the last three 0 unless `train` = xT != NULL is
- * requested by setting a->xT to any non-NULL value before the query). */
+/* bytes[0..5]: y, feat_frag, x0T, xT, masks, q4 (x0T, xT, masks 0 unless `train` = xT != NULL is
+ * requested by setting a->xT to any non-NULL value before the query; q4 0 unless a->weights is
+ * non-NULL, which also drops X3 from xT). */
 int mli_rgb_fwd_workspace(const mli_rgb_fwd_args* a, int64_t* bytes);
 
 /* ---------------------------------------------------------------- compositing
@@ -202,6 +216,8 @@ typedef struct {
   float* opacity; float* gradient; float* depth;     /* [R],[R,3],[R] (NULL to skip)      */
   float* blend_dist;      /* [R] sum_k w_k d_k (light visibility camera ray start) or NULL   */
 } mli_composite_args;
+/* y == NULL: only the weights (the heads' PQ mode needs them before the heads run); the
+ * composited outputs are then not written. */
 int mli_composite_fwd(const mli_composite_args* a, mli_stream_t s);
 
 /* Backward of the composite w.r.t. the head outputs: per-sample dZ4 = dy*y*(1-y)*scale. */
@@ -212,6 +228,8 @@ typedef struct {
   const float* d_rgb; const float* d_o_r; const float* d_o_s; const float* d_o_re;
   float grad_scale;       /* power of two, undone in mli_grad_assemble                     */
   float* dz4;             /* [N][R][8] scaled pre-sigmoid grads: rgb(3) r(3) s(1) pad       */
+  float* dray;            /* [R][8] or NULL: d loss / d composited rgb(3) o_r(3) o_s (after the
+                             o_re chain, unscaled), the per-ray factor of dz4 (mli_dw4)       */
 } mli_composite_bwd_args;
 int mli_composite_bwd(const mli_composite_bwd_args* a, mli_stream_t s);
 
@@ -224,39 +242,12 @@ typedef struct {
   const void* wbwd;       /* packed transposed weight chunks (mli_pack)                     */
   const uint32_t* masks;  /* from mli_rgb_fwd */
   uint16_t* dzT;          /* [3 heads][4 layers][256][S] feature-major dZ0..dZ3 (scaled)    */
-  uint16_t* dz4T;         /* [3 heads][4][S] feature-major dZ4 rows (scaled)                */
+  uint16_t* dz4T;         /* [3 heads][4][S] feature-major dZ4 rows (scaled), or NULL (PQ mode:
+                             the output-layer dW comes from mli_dw4)                          */
 } mli_rgb_bwd_args;
 int mli_rgb_bwd(const mli_rgb_bwd_args* a, mli_stream_t s);
 /* bytes[0..1]: dzT, dz4T. */
 int mli_rgb_bwd_workspace(const mli_rgb_bwd_args* a, int64_t* bytes);
-
-/* Fused heads backward (stage b): the dX chain of the three heads from dz4 AND the weight
- * gradients of their 256 x 256 layers 1..3 in one launch, dZ_1..dZ_3 never written to HBM;
- * replaces mli_rgb_bwd + the BIG class of mli_wgrad (autograd through MLPwithSkipConnection,
- * nerf_util.py:186-196).  Also writes dZ_0 rows and dz4 rows, the operands of the layer-0
- * (WIDE) and layer-4 (THIN) weight gradients, which stay with mli_wgrad (dZ_0 by a second launch
- * from the dZ_1 fragments the first one writes to dz1f).  Workgroup (head, l)
- * owns dW_l over a k-slice of 128-sample tiles; split[l-1] workgroups per head and l (0:
- * default 48, 24, 12).  Default: the k-slices add into dw/db (caller-zeroed) by fp32 atomics;
- * deterministic: per-slice slabs in `workspace`, summed in slice order (overwrites dw/db). */
-typedef struct {
-  int R, N;               /* S = R*N, multiple of 128 */
-  const float* dz4;       /* [N][R][8] (mli_composite_bwd) */
-  const void* wbwd;       /* mli_pack backward image (3 heads x 32 chunks) */
-  const uint32_t* masks;  /* [3][4][S/32][64][4] from mli_rgb_fwd (training) */
-  const uint16_t* xT;     /* [3][4][256][S] from mli_rgb_fwd (training) */
-  uint16_t* dz0T;         /* out [3][256][S] feature-major dZ_0 (scaled) */
-  uint16_t* dz4T;         /* out [3][4][S] feature-major dz4 rows (scaled) */
-  uint16_t* dz1f;         /* scratch [3][S/32][16][64][8]: dZ_1 as MFMA B fragments (bytes[3]) */
-  float* dw[9];           /* [head*3 + l-1]: dW_l [256][256] (row = output feature) */
-  float* db[9];           /* [head*3 + l-1]: db_l [256] */
-  int split[3];
-  int deterministic;
-  float* workspace;       /* deterministic: bytes[2] of mli_heads_bwd_workspace */
-} mli_heads_bwd_args;
-int mli_heads_bwd(const mli_heads_bwd_args* a, mli_stream_t s);
-/* bytes[0..3]: dz0T, dz4T, workspace (0 unless deterministic), dz1f.  S must be a multiple of 256. */
-int mli_heads_bwd_workspace(const mli_heads_bwd_args* a, int64_t* bytes);
 
 /* Weight/bias gradients dW_l = dZ_l^T X_l, db_l = sum dZ_l (split-K MFMA GEMM).  Default: the
  * k-slices add into dw/db (caller-zeroed) by fp32 atomics, in arbitrary order.  deterministic:
@@ -290,6 +281,26 @@ typedef struct {
 int mli_wgrad(const mli_wgrad_args* a, mli_stream_t s);
 /* bytes[0]: workspace (0 unless deterministic): the largest class in `classes`. */
 int mli_wgrad_workspace(const mli_wgrad_args* a, int64_t* bytes);
+
+/* Output-layer weight / bias gradients of the heads from the forward's partials (PQ mode of
+ * mli_rgb_fwd): dW4[c][f] = scale * sum_(wg,seg) dray[ray(wg,seg)][off_h + c] * q4[wg][seg][h][f][c],
+ * db4[c] the same over row 256, off_h = 3h.  Replaces the THIN mli_wgrad class (the autograd dW /
+ * db of the last nn.Linear of each MLPwithSkipConnection, nerf_util.py:186-196).  Two launches:
+ * per-slice partial sums into the workspace, then a sum over the slices in slice order
+ * (bit-reproducible; dw / db overwritten). */
+typedef struct {
+  int R, N, n_heads;      /* S = R*N, N % 32 == 0 */
+  const float* q4;        /* [S/256][MLI_Q4_SEGS(N)][n_heads][257][4] from mli_rgb_fwd */
+  const float* dray;      /* [R][8] */
+  float scale;            /* grad_scale / MLI_Q4_SCALE (the dw / db land at the split-K dW scale) */
+  float* dw[3];           /* per head: [k_out][256] */
+  float* db[3];           /* per head: [k_out] */
+  int k_out[3];           /* 3, 3, 1 (LumenRGB 'rgb_r_s') */
+  float* workspace;       /* bytes[0] */
+} mli_dw4_args;
+int mli_dw4(const mli_dw4_args* a, mli_stream_t s);
+/* bytes[0]: workspace (slice partials). */
+int mli_dw4_workspace(const mli_dw4_args* a, int64_t* bytes);
 
 /* ---------------------------------------------------------------- stage a (geometry training)
  * Backward of the whole render w.r.t. the geometry: replaces autograd through
@@ -511,6 +522,7 @@ typedef struct {
   int defer_finalize;      /* 1: leave the loss values to mli_composite_loss_finalize (the
                               gradients do not need them; the host issues it where the GPU is
                               idle, e.g. after the weight gradients)                           */
+  float* dray;             /* [R][8] or NULL, as mli_composite_bwd_args                         */
 } mli_composite_loss_args;
 int mli_composite_loss(const mli_composite_loss_args* a, mli_stream_t s);
 /* The loss values of a deferred mli_composite_loss (same args, same scratch). */

@@ -51,7 +51,7 @@ class SampleFineArgs(C.Structure):
 class RgbFwdArgs(C.Structure):
     _fields_ = [("R", I32), ("N", I32), ("center", P), ("ray_unit", P), ("pts_light", P),
                 ("dists", P), ("grad", P), ("h0", P), ("wfwd", P), ("y", P), ("feat_frag", P),
-                ("x0T", P), ("xT", P), ("masks", P), ("n_heads", I32)]
+                ("x0T", P), ("xT", P), ("masks", P), ("n_heads", I32), ("weights", P), ("q4", P)]
 
 
 class CompositeArgs(C.Structure):
@@ -64,18 +64,12 @@ class CompositeArgs(C.Structure):
 class CompositeBwdArgs(C.Structure):
     _fields_ = [("R", I32), ("N", I32), ("weights", P), ("y", P), ("o_r", P), ("o_s", P),
                 ("d_rgb", P), ("d_o_r", P), ("d_o_s", P), ("d_o_re", P), ("grad_scale", F32),
-                ("dz4", P)]
+                ("dz4", P), ("dray", P)]
 
 
 class RgbBwdArgs(C.Structure):
     _fields_ = [("R", I32), ("N", I32), ("dz4", P), ("wbwd", P), ("masks", P), ("dzT", P),
                 ("dz4T", P)]
-
-
-class HeadsBwdArgs(C.Structure):
-    _fields_ = [("R", I32), ("N", I32), ("dz4", P), ("wbwd", P), ("masks", P), ("xT", P), ("dz0T", P),
-                ("dz4T", P), ("dz1f", P), ("dw", P * 9), ("db", P * 9), ("split", I32 * 3), ("deterministic", I32),
-                ("workspace", P)]
 
 
 class WgradJob(C.Structure):
@@ -85,6 +79,14 @@ class WgradJob(C.Structure):
 class WgradArgs(C.Structure):
     _fields_ = [("S", I32), ("n_jobs", I32), ("jobs", P), ("classes", I32), ("deterministic", I32),
                 ("workspace", P)]
+
+
+class Dw4Args(C.Structure):
+    _fields_ = [("R", I32), ("N", I32), ("n_heads", I32), ("q4", P), ("dray", P), ("scale", F32),
+                ("dw", P * 3), ("db", P * 3), ("k_out", I32 * 3), ("workspace", P)]
+
+
+Q4_SCALE = 65536.0  # include/mli_hip.h MLI_Q4_SCALE
 
 
 class LossArgs(C.Structure):
@@ -100,7 +102,7 @@ class LossArgs(C.Structure):
 
 class CompositeLossArgs(C.Structure):
     _fields_ = [("comp", CompositeArgs), ("loss", LossArgs), ("grad_scale", F32), ("dz4", P),
-                ("defer_finalize", I32)]
+                ("defer_finalize", I32), ("dray", P)]
 
 class PackLayer(C.Structure):
     _fields_ = [("v", P), ("g", P), ("bias", P), ("n_out", I32), ("k_ref", I32), ("transpose", I32),
@@ -185,14 +187,14 @@ class FragRowsArgs(C.Structure):
                 ("ld", I64), ("col0", I64), ("row0", I32)]
 
 
-ABI_VERSION = 11  # include/mli_hip.h MLI_ABI_VERSION
+ABI_VERSION = 12  # include/mli_hip.h MLI_ABI_VERSION
 
 ENTRY_POINTS = {
     "mli_rays": RaysArgs, "mli_hashgrid_fwd": HashgridArgs, "mli_sdf": SdfArgs,
     "mli_sample_coarse": SampleCoarseArgs, "mli_sample_fine": SampleFineArgs,
     "mli_rgb_fwd": RgbFwdArgs, "mli_composite_fwd": CompositeArgs,
-    "mli_composite_bwd": CompositeBwdArgs, "mli_rgb_bwd": RgbBwdArgs, "mli_heads_bwd": HeadsBwdArgs,
-    "mli_wgrad": WgradArgs,
+    "mli_composite_bwd": CompositeBwdArgs, "mli_rgb_bwd": RgbBwdArgs,
+    "mli_wgrad": WgradArgs, "mli_dw4": Dw4Args,
     "mli_pack": PackArgs, "mli_pack_sdf": PackSdfArgs, "mli_grad_assemble": AssembleArgs,
     "mli_adamw": AdamwArgs, "mli_cast_f16": CastArgs, "mli_stage_b_loss": LossArgs,
     "mli_composite_bwd_geo": CompositeBwdGeoArgs, "mli_geo_bwd": GeoBwdArgs, "mli_sdf_bwd": SdfBwdArgs,
@@ -204,9 +206,9 @@ ENTRY_POINTS = {
 # host-only scratch-size queries: int mli_<op>_workspace(const args*, int64_t* bytes) -> how many
 # sizes each writes (include/mli_hip.h lists their order)
 WORKSPACE = {
-    "mli_sdf": 1, "mli_rgb_fwd": 5, "mli_rgb_bwd": 2, "mli_wgrad": 1, "mli_composite_bwd_geo": 4,
+    "mli_sdf": 1, "mli_rgb_fwd": 6, "mli_rgb_bwd": 2, "mli_wgrad": 1, "mli_composite_bwd_geo": 4,
     "mli_geo_bwd": 6, "mli_sdf_bwd": 4, "mli_hash_bwd": 1, "mli_light_visibility": 5, "mli_stage_b_loss": 5,
-    "mli_pack": 1, "mli_heads_bwd": 4, "mli_composite_loss": 2,
+    "mli_pack": 1, "mli_dw4": 1, "mli_composite_loss": 2,
 }
 
 _lib = None

@@ -10,12 +10,10 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmli_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["rays.hip", "sdf.hip", "mlp.hip", "heads_bwd.hip", "wgrad.hip", "params.hip", "loss.hip"]
+SOURCES = ["rays.hip", "sdf.hip", "mlp.hip", "wgrad.hip", "params.hip", "loss.hip"]
 # sdf.hip: no SLP packing, so fma(fp16 -> fp32 feature, w, acc) selects v_fma_mix_f32 (one
 # instruction) instead of v_cvt_f32_f16 x2 + v_pk_fma_f32
-# heads_bwd.hip: the dW accumulators live in AGPRs through asm constraints; the compiler's own
-# (chain) MFMAs must then take the VGPR form
-PER_FILE = {"sdf.hip": ["-fno-slp-vectorize"], "heads_bwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+PER_FILE = {"sdf.hip": ["-fno-slp-vectorize"]}
 FLAGS = ["-O3", "--offload-arch=gfx950", "-fPIC", "-std=c++17", "-ffp-contract=off",
          "-I", os.path.join(REPO, "include"), "-I", CSRC]
 

@@ -59,6 +59,9 @@ struct Geo {
   static constexpr int MASK_OFF = STAGE_OFF + 2 * STAGE;
   static constexpr int LDS_FWD = STAGE_OFF + 2 * STAGE;
   static constexpr int LDS_BWD = MASK_OFF + 2 * MASKB;
+  // per-wave transpose scratch of the output-layer partials (rgb_fwd PQ mode, q4_tile)
+  static constexpr int PQ_WAVE = 2048 + 256;
+  static constexpr int LDS_FWD_PQ = LDS_FWD + NW * PQ_WAVE;
   static constexpr int TPR = SAMPLES / 8;  // 16 B flush pieces per staged row
   // ring DMAs per wave and chunk, flush stores per wave and staged tile
   template <int ROLE> static constexpr int ring_ops() { return ROLE == STORE ? 0 : RND; }
@@ -245,12 +248,122 @@ struct NoPre {
   MLI_FI void issue(int) const {}
 };
 
+// ---------------------------------------------------------------------- output-layer partials
+// PQ mode (stage b): the output layer's weight gradient factors through the per-ray loss
+// gradient.  The composited outputs are sums over a ray's samples, out_rc = sum_s w_s y_sc (+ bg),
+// with weights w_s that do not depend on the heads, so d loss / d z4_sc = D_rc w_s y_sc (1 - y_sc)
+// with D_rc = d loss / d out_rc (after the o_re chain).  Hence
+//   dW4[c, :] = sum_s dz4_cs X3[:, s] = sum_tiles D[r(tile), c] Q[tile, c, :],
+//   Q[tile, c, f] = sum_{s in tile} g_sc X3[f, s],   g_sc = w_s y_sc (1 - y_sc),
+// and Q is formed here while X3 (the output layer's input) is still in registers: X3 never
+// goes to HBM and the THIN dW GEMM that read it back is gone (mli_dw4 contracts Q with D).
+// The tile's 32 samples belong to one ray (N % 32 == 0).
+//
+// Per 32-feature block: the wave's X3 fragments go to a wave-private LDS block as
+// [32 samples][32 features] (8 B chunks XOR-swizzled by row: conflict-free b64 writes and
+// transposed reads), ds_read_b64_tr_b16 returns them as B fragments with samples along k, and
+// two MFMAs contract them with G^T [c][samples] (rows 0..2 = g of the head's outputs, scaled by
+// MLI_Q4_SCALE into fp16 range; rows >= 3 zero).  Lane (f, h = 0) then holds Q[c = 0..3][f].
+// Each wave parks its Q (257 rows of f32x4, the last one sum_s g_sc) in the free staging area;
+// after a barrier the STORE waves sum the waves of each ray segment of the workgroup in wave
+// order (fixed order: bit-reproducible) and write q4[wg][seg] -- N = 128: two rays per workgroup,
+// a quarter of the per-tile partials -- and a second barrier frees the staging area again.
+constexpr float Q4_SCALE = MLI_Q4_SCALE;  // g <= 1/4 -> fp16 <= 16384 (undone through mli_dw4 scale)
+constexpr int Q4_SLOT = 257 * 16;          // one wave's Q in LDS
+
+template <class G, int ROLE>
+MLI_FI void q4_tile(const mli_rgb_fwd_args& a, uint8_t* lds, const half8 (&X)[19], const float (&gq)[3], int hd,
+                    int lane) {
+  static_assert(G::NW * Q4_SLOT <= 2 * G::STAGE, "Q slots in the staging area");
+  const int wave = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
+  uint8_t* xr = lds + G::LDS_FWD + wave * G::PQ_WAVE;
+  uint8_t* gr = xr + 2048;
+  uint8_t* qs = lds + G::STAGE_OFF + wave * Q4_SLOT;
+  // G^T rows 0..3 (row 3 zero) from the lanes that hold the outputs
+  if (h == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<f16*>(gr + i * 64 + c * 2) = (f16)(i < 3 ? gq[i] : 0.f);
+  }
+  asm volatile("" ::: "memory");
+  half8 gf[2];
+  {
+    const int gi = min(c, 3);  // rows >= 3 read the zero row
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) gf[ks] = *reinterpret_cast<const half8*>(gr + gi * 64 + (16 * ks + 8 * h) * 2);
+  }
+  // transposed-read addressing: 16-lane group g16 covers features 16 (g16 & 1) .. + 15 of lane
+  // half g16 >> 1; lane 4q + p of a group reads row (sample) q of the 4, chunk p of its 16 features
+  const int g16 = (lane >> 4) & 3, q = (lane & 15) >> 2, p = lane & 3;
+  const int chunk = 4 * (g16 & 1) + p;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    // X3 features 32b .. 32b+31 of sample c: fragment element j of k-step 2b + u is feature
+    // 16u + 8(j >> 2) + 4h + (j & 3) of the block -> 8 B chunk 4u + 2(j >> 2) + h
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const u32x4 w = __builtin_bit_cast(u32x4, X[2 * b + u]);
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int ch = (4 * u + 2 * jj + h) ^ ((c >> 1) & 7);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(xr + c * 64 + ch * 8);
+        *reinterpret_cast<uint2*>(dst) = make_uint2(w[2 * jj], w[2 * jj + 1]);
+      }
+    }
+    asm volatile("" ::: "memory");
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int s0 = 16 * ks + 8 * h + q, s1 = s0 + 4;
+      const half4 lo = ds_read_tr16(xr + s0 * 64 + (chunk ^ ((s0 >> 1) & 7)) * 8);
+      const half4 hi = ds_read_tr16(xr + s1 * 64 + (chunk ^ ((s1 >> 1) & 7)) * 8);
+      half8 xf;
+      xf[0] = lo[0]; xf[1] = lo[1]; xf[2] = lo[2]; xf[3] = lo[3];
+      xf[4] = hi[0]; xf[5] = hi[1]; xf[6] = hi[2]; xf[7] = hi[3];
+      acc = mfma32(gf[ks], xf, acc);
+    }
+    asm volatile("" ::: "memory");  // the next block's writes stay behind these reads
+    if (h == 0) *reinterpret_cast<f32x4*>(qs + (32 * b + c) * 16) = f32x4{acc[0], acc[1], acc[2], acc[3]};
+  }
+  // bias row 256: sum_s g_sc (fp32)
+  float sb[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    float v = gq[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    sb[i] = v;
+  }
+  if (lane == 0) *reinterpret_cast<f32x4*>(qs + 256 * 16) = f32x4{sb[0], sb[1], sb[2], 0.f};
+  block_sync();
+  if (ROLE != DMA) {
+    // ray segments of the workgroup: tile t holds ray 32 t / N
+    const int N = a.N, t0 = blockIdx.x * G::NW;
+    const int r_first = t0 * 32 / N;
+    const int nseg = ((t0 + G::NW) * 32 - 1) / N - r_first + 1;
+    const int segs = MLI_Q4_SEGS(N);
+    const int nthr = ROLE == STORE ? G::THREADS / 2 : G::THREADS;
+    const int tid = ROLE == STORE ? threadIdx.x - G::THREADS / 2 : threadIdx.x;
+    f32x4* qo = reinterpret_cast<f32x4*>(a.q4) + (size_t)blockIdx.x * segs * a.n_heads * 257;
+    for (int it = tid; it < nseg * 257; it += nthr) {
+      const int seg = it / 257, row = it - seg * 257;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int w = 0; w < G::NW; ++w)
+        if ((t0 + w) * 32 / N - r_first == seg) v += *reinterpret_cast<const f32x4*>(lds + G::STAGE_OFF + w * Q4_SLOT + row * 16);
+      __builtin_nontemporal_store(v, qo + ((size_t)seg * a.n_heads + hd) * 257 + row);
+    }
+  }
+  block_sync();  // the staging area is free again
+}
+
 // ---------------------------------------------------------------------- forward
 // chunk sizes in consumption order: SDF layer 1 (8 x KS 16), then per head L0 (8 x KS 19),
 // L1..L3 (24 x KS 16), L4 (1 x KS 16)
 MLI_FI int fwd_bytes(int c) { return (c >= 8 && (c - 8) % 33 < 8) ? CH(19) : CH(16); }
 
-template <class G, bool TRAIN, int ROLE>
+template <class G, bool TRAIN, bool PQ, int ROLE>
 MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
@@ -260,6 +373,8 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
   const int r = m / a.N, k = m - r * a.N;
   const size_t slot = (size_t)k * a.R + r;
   auto bytes = [](int cc) MLI_LAMBDA_FI { return fwd_bytes(cc); };
+  constexpr int XL = PQ ? 3 : 4;  // activation layers stored per head (PQ: X3 is not)
+  const float wgt = PQ ? a.weights[slot] : 0.f;  // composite weight of the sample (PQ)
 
   Ring rg;
   ring_start(rg, a.wfwd, 8 + a.n_heads * 33, bytes);
@@ -340,8 +455,9 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
       for (int q = 0; q < 16; ++q) B[q] = src[q * 64];
     }
     uint32_t mbits[4];
-    auto relu_epi = [&](half8* out, int layer) MLI_LAMBDA_FI {
-      return [&, out, layer](int t, const f32x16& acc) MLI_LAMBDA_FI {
+    // stg: the layer's activations go to xT (PQ: not X3, the output layer's input)
+    auto relu_epi = [&](half8* out, int layer, bool stg) MLI_LAMBDA_FI {
+      return [&, out, layer, stg](int t, const f32x16& acc) MLI_LAMBDA_FI {
         f32x16 v;
 #pragma unroll
         for (int i = 0; i < 16; ++i) v[i] = relu1(acc[i]);
@@ -352,8 +468,9 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
 #pragma unroll
           for (int i = 0; i < 16; ++i) bits |= (acc[i] > 0.0f ? 1u : 0u) << i;
           if (t & 1) mbits[t >> 1] |= bits << 16; else mbits[t >> 1] = bits;
-          stage_tile<G>(sg, lds, out[2 * t], out[2 * t + 1],
-                        a.xT + ((size_t)(hd * 4 + layer) * 256 + 32 * t) * S + col0, lane);
+          if (stg)
+            stage_tile<G>(sg, lds, out[2 * t], out[2 * t + 1],
+                          a.xT + ((size_t)(hd * XL + layer) * 256 + 32 * t) * S + col0, lane);
           if (t == 7) {
             u32x4* mp = reinterpret_cast<u32x4*>(a.masks) +
                         ((size_t)(hd * 4 + layer) * (S / 32) + tile) * 64 + lane;
@@ -362,20 +479,28 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
         }
       };
     };
-    run_layer<G, ROLE, 19, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, B, lane, bytes, NoPre{}, relu_epi(A, 0));
-    run_layer<G, ROLE, 16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, A, lane, bytes, NoPre{}, relu_epi(B, 1));
-    run_layer<G, ROLE, 16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, B, lane, bytes, NoPre{}, relu_epi(A, 2));
-    run_layer<G, ROLE, 16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, A, lane, bytes, NoPre{}, relu_epi(B, 3));
+    run_layer<G, ROLE, 19, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, B, lane, bytes, NoPre{}, relu_epi(A, 0, true));
+    run_layer<G, ROLE, 16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, A, lane, bytes, NoPre{}, relu_epi(B, 1, true));
+    run_layer<G, ROLE, 16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, B, lane, bytes, NoPre{}, relu_epi(A, 2, true));
+    run_layer<G, ROLE, 16, 8, TRAIN && !PQ, 0, TRAIN>(rg, lds, sg, S, A, lane, bytes, NoPre{},
+                                                      relu_epi(B, 3, !PQ));
     const int no = hd == 2 ? 1 : 3;
     const int off = hd * 3;
+    float gq[3] = {0.f, 0.f, 0.f};
     run_layer<G, ROLE, 16, 1, false, 0, false>(rg, lds, sg, S, B, lane, bytes, NoPre{},
                                       [&](int, const f32x16& acc) MLI_LAMBDA_FI {
       if (h == 0) {
 #pragma unroll
         for (int i = 0; i < 3; ++i)
-          if (i < no) a.y[8 * slot + off + i] = sigmoidf_acc(acc[i]);
+          if (i < no) {
+            const float y = sigmoidf_acc(acc[i]);
+            a.y[8 * slot + off + i] = y;
+            if (PQ) gq[i] = Q4_SCALE * wgt * (y * (1.0f - y));
+          }
       }
     });
+    // (the q4 stores come from the STORE waves only: the DMA waves' counted waits are unchanged)
+    if (PQ) q4_tile<G, ROLE>(a, lds, B, gq, hd, lane);
   }
   vm_wait(0);  // no LDS-DMA may land after the workgroup's LDS is released
 }
@@ -390,11 +515,11 @@ typedef Geo<8, 17, true> GBwd;
 
 // the first / second half of the waves take the DMA / STORE roles (see Role), compiled as two
 // programs
-template <bool TRAIN>
+template <bool TRAIN, bool PQ>
 __global__ __launch_bounds__(GFwd::THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= GFwd::NW / 2) rgb_fwd_body<GFwd, TRAIN, STORE>(a, lds);
-  else rgb_fwd_body<GFwd, TRAIN, DMA>(a, lds);
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= GFwd::NW / 2) rgb_fwd_body<GFwd, TRAIN, PQ, STORE>(a, lds);
+  else rgb_fwd_body<GFwd, TRAIN, PQ, DMA>(a, lds);
 }
 
 // ---------------------------------------------------------------------- backward dX chain
@@ -453,7 +578,8 @@ MLI_FI void rgb_bwd_body(const mli_rgb_bwd_args& a, uint8_t* lds) {
           if (j < no) {
             const f16 zj = (f16)dz[j];  // never bit_cast a vector element (yields element 0)
             z4[j] = zj;
-            a.dz4T[((size_t)hd * 4 + j) * S + m] = __builtin_bit_cast(uint16_t, zj);
+            // the THIN dW operand (NULL: the output-layer dW comes from the forward's partials)
+            if (a.dz4T) a.dz4T[((size_t)hd * 4 + j) * S + m] = __builtin_bit_cast(uint16_t, zj);
           }
       }
     }
@@ -500,87 +626,6 @@ __global__ __launch_bounds__(GBwd::THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args
   else rgb_bwd_body<GBwd, DMA>(a, lds);
 }
 
-
-// ---------------------------------------------------------------------- dZ_0 from dZ_1 fragments
-// Second launch of mli_heads_bwd: per head dZ_0 = (W1^T dZ_1) * relu'(Z_0) (nerf_util.py:186-196
-// autograd), B operand = the dZ_1 fragment image heads_bwd_kernel wrote, W1^T = the last 8
-// chunks of each head in the mli_pack bwd image, written as feature-major rows (the operand of
-// the layer-0 dW).  One workgroup = 256 samples, as mli_rgb_bwd.
-constexpr int HB_HEAD_BYTES = 8 * CH(1) + 24 * CH(16);
-
-typedef Geo<8, 17, true> GDz0;
-
-template <int ROLE>
-MLI_FI void dz0_body(const mli_heads_bwd_args& a, uint8_t* lds) {
-  typedef GDz0 G;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int tiles = a.R * a.N / 32;
-  const int tile = blockIdx.x * G::NW + wave;
-  ChunkAt at{reinterpret_cast<const uint8_t*>(a.wbwd), HB_HEAD_BYTES, 8 * CH(1) + 16 * CH(16)};
-  constexpr int MASK_OPS = ROLE == DMA ? 2 : 0;
-  // ReLU masks of head layer 0 of head hd (the workgroup's 8 tiles, 8 KiB) into slot hd & 1
-  auto mask_dma = [&](int hd) MLI_LAMBDA_FI {
-    const int hc = min(hd, 2);
-    const uint8_t* src = reinterpret_cast<const uint8_t*>(a.masks) +
-                         (((size_t)(hc * 4) * tiles + (size_t)blockIdx.x * G::NW) * 64) * 16;
-#pragma unroll
-    for (int u = 0; u < MASK_OPS; ++u)
-      glds16(src + u * (G::MASKB / 2) + threadIdx.x * 16,
-             lds + G::MASK_OFF + (hd & 1) * G::MASKB + u * (G::MASKB / 2) + wave * 1024);
-  };
-  Ring rg;
-  rg.src = rg.last = nullptr;
-  rg.next = 0;
-  rg.n = 24;
-  rg.cur = 0;
-  mask_dma(0);
-#pragma unroll
-  for (int d = 0; d < DIST; ++d) ring_issue<G, ROLE>(rg, lds, at);
-  if (ROLE != STORE) vm_wait((DIST - 1) * G::template ring_ops<ROLE>());
-  block_sync();
-
-  half8 B[16];
-  Stager sg{nullptr, 0, 0};
-  const size_t col0 = (size_t)blockIdx.x * G::SAMPLES;
-  for (int hd = 0; hd < 3; ++hd) {
-    const int S = opaque_s(a.R * a.N);
-    {
-      const half8* src = reinterpret_cast<const half8*>(a.dz1f + (size_t)hd * 256 * S) +
-                         (size_t)tile * 16 * 64 + opaque_v(lane);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) B[q] = src[q * 64];
-    }
-    struct MaskPre {
-      decltype(mask_dma)& dma;
-      int next_head;
-      MLI_FI int count(int t) const { return t == 8 - DIST ? MASK_OPS : 0; }
-      MLI_FI void issue(int t) const {
-        if (t == 8 - DIST) dma(next_head);
-      }
-    };
-    run_layer<G, ROLE, 16, 8, true, 0, false>(rg, lds, sg, S, B, lane, at, MaskPre{mask_dma, hd + 1},
-                                          [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
-      const u32x4 mv =
-          *reinterpret_cast<const u32x4*>(lds + G::MASK_OFF + (hd & 1) * G::MASKB + wave * 1024 + lane * 16);
-      const int wi = t >> 1;
-      const uint32_t word = wi == 0 ? mv[0] : wi == 1 ? mv[1] : wi == 2 ? mv[2] : mv[3];
-      const uint32_t bits = word >> ((t & 1) * 16);
-      f32x16 v;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = ((bits >> i) & 1u) ? acc[i] : 0.0f;
-      stage_tile<G>(sg, lds, acc_to_frag(v, 0), acc_to_frag(v, 1), a.dz0T + ((size_t)hd * 256 + 32 * t) * S + col0,
-                    lane);
-    });
-  }
-  stage_flush<G, ROLE>(sg, lds, opaque_s(a.R * a.N));
-  vm_wait(0);
-}
-
-__global__ __launch_bounds__(GDz0::THREADS) void dz0_kernel(mli_heads_bwd_args a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 8)) dz0_body<STORE>(a, lds);
-  else dz0_body<DMA>(a, lds);
-}
 
 // ---------------------------------------------------------------------- stage a: geometry dX chain
 // The single 'rgb' head (NeuralLumen/utils/modules.py:164-174) backward down to its inputs,
@@ -721,27 +766,23 @@ __global__ __launch_bounds__(GGeo::THREADS) void geo_bwd_kernel(mli_geo_bwd_args
 
 }  // namespace
 
-namespace mli_detail {
-int heads_dz0_launch(const mli_heads_bwd_args* a, hipStream_t s) {
-  const int S = a->R * a->N;
-  if (S % 256 != 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(dz0_kernel, dim3(S / GDz0::SAMPLES), dim3(GDz0::THREADS), GDz0::LDS_BWD, s, *a);
-  return (int)hipGetLastError();
-}
-}  // namespace mli_detail
-
 extern "C" int mli_rgb_fwd(const mli_rgb_fwd_args* a, mli_stream_t s) {
   const int S = a->R * a->N;
   if (S % 256 != 0) return (int)hipErrorInvalidValue;
   const bool train = a->xT != nullptr;
   if (train && (a->x0T == nullptr || a->masks == nullptr)) return (int)hipErrorInvalidValue;
   if (a->n_heads != 1 && a->n_heads != 3) return (int)hipErrorInvalidValue;
-  if (train)
-    hipLaunchKernelGGL(rgb_fwd_kernel<true>, dim3(S / GFwd::SAMPLES), dim3(GFwd::THREADS), GFwd::LDS_FWD,
-                       (hipStream_t)s, *a);
+  // output-layer partials: training only, one ray per 32-sample tile, both pointers or none
+  const bool pq = a->weights != nullptr;
+  if (pq && (!train || a->q4 == nullptr || a->N % 32 != 0)) return (int)hipErrorInvalidValue;
+  if (!pq && a->q4 != nullptr) return (int)hipErrorInvalidValue;
+  const dim3 grid(S / GFwd::SAMPLES), block(GFwd::THREADS);
+  if (pq)
+    hipLaunchKernelGGL((rgb_fwd_kernel<true, true>), grid, block, GFwd::LDS_FWD_PQ, (hipStream_t)s, *a);
+  else if (train)
+    hipLaunchKernelGGL((rgb_fwd_kernel<true, false>), grid, block, GFwd::LDS_FWD, (hipStream_t)s, *a);
   else
-    hipLaunchKernelGGL(rgb_fwd_kernel<false>, dim3(S / GFwd::SAMPLES), dim3(GFwd::THREADS), GFwd::LDS_FWD,
-                       (hipStream_t)s, *a);
+    hipLaunchKernelGGL((rgb_fwd_kernel<false, false>), grid, block, GFwd::LDS_FWD, (hipStream_t)s, *a);
   MLI_LAUNCH_CHECK();
 }
 
@@ -756,11 +797,14 @@ extern "C" int mli_rgb_bwd(const mli_rgb_bwd_args* a, mli_stream_t s) {
 extern "C" int mli_rgb_fwd_workspace(const mli_rgb_fwd_args* a, int64_t* bytes) {
   const int64_t S = (int64_t)a->R * a->N;
   if (S <= 0 || S % 256 != 0 || (a->n_heads != 1 && a->n_heads != 3)) return (int)hipErrorInvalidValue;
+  const bool pq = a->weights != nullptr;
+  if (pq && a->N % 32 != 0) return (int)hipErrorInvalidValue;
   bytes[0] = S * 8 * 4;                                   // y
   bytes[1] = S * 256 * 2;                                 // feat_frag
   bytes[2] = (int64_t)MLI_HEAD_K0 * S * 2;                // x0T (training)
-  bytes[3] = (int64_t)a->n_heads * 4 * 256 * S * 2;       // xT (training)
+  bytes[3] = (int64_t)a->n_heads * (pq ? 3 : 4) * 256 * S * 2;  // xT (training)
   bytes[4] = (int64_t)a->n_heads * 4 * (S / 32) * 64 * 16;  // masks (training)
+  bytes[5] = pq ? (S / 256) * MLI_Q4_SEGS(a->N) * a->n_heads * 257 * 4 * 4 : 0;  // q4 (PQ)
   return 0;
 }
 

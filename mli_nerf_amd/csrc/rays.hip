@@ -338,6 +338,7 @@ MLI_FI void composite_ray(const mli_composite_args& a, int r, int lane, float (&
     if (k < N) {
       const size_t s = (size_t)k * R + r;
       a.weights[s] = wv[e];
+      if (a.y == nullptr) continue;  // weights only (mli_composite_fwd, PQ heads)
       const f32x4 y0 = *reinterpret_cast<const f32x4*>(a.y + 8 * s);
       const f32x4 y1 = *reinterpret_cast<const f32x4*>(a.y + 8 * s + 4);
       yk[e][0] = y0[0]; yk[e][1] = y0[1]; yk[e][2] = y0[2]; yk[e][3] = y0[3];
@@ -380,7 +381,7 @@ __global__ __launch_bounds__(CW * 64) void composite_fwd_kernel(mli_composite_ar
   if (r >= a.R) return;  // the ray's lanes exit together (no block barriers below)
   float wv[CE], yk[CE][7], acc[12];
   composite_ray<L>(a, r, sub, wv, yk, acc);
-  if (sub != 0) return;
+  if (sub != 0 || a.y == nullptr) return;
   float rgb[3], orr[3], os, ore[3];
   composite_outputs(a, acc, rgb, orr, os, ore);
   for (int i = 0; i < 3; ++i) {
@@ -395,28 +396,37 @@ __global__ __launch_bounds__(CW * 64) void composite_fwd_kernel(mli_composite_ar
   if (a.blend_dist) a.blend_dist[r] = acc[11];  // render.composite(dists, weights)
 }
 
-// d total / d (rgb, o_r, o_s, o_re) of one ray -> the per-sample pre-sigmoid gradients (scaled)
-// of its samples: the composite + o_re + sigmoid backward (one definition for both paths).
-MLI_FI void composite_bwd_sample(const float (&dr_in)[3], const float (&dor_in)[3], float d_o_s,
-                                 const float (&d_o_re)[3], const float (&orr)[3], float os, float w,
-                                 const float (&y)[7], f32x4& o0, f32x4& o1) {
-  float dr[3], dor[3];
+// d total / d (rgb, o_r, o_s, o_re) of one ray -> d total / d composited rgb, o_r, o_s once the
+// o_re = rgb - o_r * o_s chain is folded in (NeuralLumen/model.py:305): the per-ray factor D of
+// every sample's pre-sigmoid gradient (written as `dray` for mli_dw4).
+MLI_FI void ray_dz(const float (&dr_in)[3], const float (&dor_in)[3], float d_o_s, const float (&d_o_re)[3],
+                   const float (&orr)[3], float os, float (&D)[7]) {
   float sre = 0.f;
   for (int i = 0; i < 3; ++i) {
     const float dre = d_o_re[i];
-    dr[i] = dr_in[i] + dre;
-    dor[i] = dor_in[i] - dre * os;
+    D[i] = dr_in[i] + dre;
+    D[3 + i] = dor_in[i] - dre * os;
     sre += dre * orr[i];
   }
-  const float dos = d_o_s - sre;
-  o0[0] = w * dr[0] * (y[0] * (1.f - y[0]));
-  o0[1] = w * dr[1] * (y[1] * (1.f - y[1]));
-  o0[2] = w * dr[2] * (y[2] * (1.f - y[2]));
-  o0[3] = w * dor[0] * (y[3] * (1.f - y[3]));
-  o1[0] = w * dor[1] * (y[4] * (1.f - y[4]));
-  o1[1] = w * dor[2] * (y[5] * (1.f - y[5]));
-  o1[2] = w * dos * (y[6] * (1.f - y[6]));
+  D[6] = d_o_s - sre;
+}
+
+// The per-sample pre-sigmoid gradients (scaled) of a ray's samples from its D: the composite +
+// sigmoid backward (one definition for both paths).
+MLI_FI void composite_bwd_sample(const float (&D)[7], float w, const float (&y)[7], f32x4& o0, f32x4& o1) {
+  o0[0] = w * D[0] * (y[0] * (1.f - y[0]));
+  o0[1] = w * D[1] * (y[1] * (1.f - y[1]));
+  o0[2] = w * D[2] * (y[2] * (1.f - y[2]));
+  o0[3] = w * D[3] * (y[3] * (1.f - y[3]));
+  o1[0] = w * D[4] * (y[4] * (1.f - y[4]));
+  o1[1] = w * D[5] * (y[5] * (1.f - y[5]));
+  o1[2] = w * D[6] * (y[6] * (1.f - y[6]));
   o1[3] = 0.f;
+}
+
+MLI_FI void store_dray(float* dray, int r, const float (&D)[7]) {
+  *reinterpret_cast<f32x4*>(dray + 8 * r) = f32x4{D[0], D[1], D[2], D[3]};
+  *reinterpret_cast<f32x4*>(dray + 8 * r + 4) = f32x4{D[4], D[5], D[6], 0.f};
 }
 
 // Fused stage-b training tail, one wave per ray: composite (as composite_fwd_kernel), the loss
@@ -461,6 +471,9 @@ __global__ __launch_bounds__(CW * 64) void composite_loss_kernel(mli_composite_l
       acc[0] = ra[0]; acc[1] = ra[1]; acc[4] = ra[4]; acc[5] = ra[5]; acc[6] = ra[6]; acc[7] = ra[7];
     }
     const bool outside = L.outside[r] != 0;
+    float D[7];
+    ray_dz(d_rgb, d_o_r, d_o_s, d_o_re, orr, os, D);
+    if (A.dray && sub == 0) store_dray(A.dray, r, D);
 #pragma unroll
     for (int e = 0; e < CE; ++e) {
       const int k = CE * sub + e;
@@ -468,7 +481,7 @@ __global__ __launch_bounds__(CW * 64) void composite_loss_kernel(mli_composite_l
         const size_t s = (size_t)k * R + r;
         if (!outside) sample_terms(L, s, acc);
         f32x4 o0, o1;
-        composite_bwd_sample(d_rgb, d_o_r, d_o_s, d_o_re, orr, os, wv[e] * A.grad_scale, yk[e], o0, o1);
+        composite_bwd_sample(D, wv[e] * A.grad_scale, yk[e], o0, o1);
         *reinterpret_cast<f32x4*>(A.dz4 + 8 * s) = o0;
         *reinterpret_cast<f32x4*>(A.dz4 + 8 * s + 4) = o1;
       }
@@ -527,8 +540,11 @@ __global__ __launch_bounds__(256) void composite_bwd_kernel(mli_composite_bwd_ar
   const f32x4 y0 = *reinterpret_cast<const f32x4*>(a.y + 8 * s);
   const f32x4 y1 = *reinterpret_cast<const f32x4*>(a.y + 8 * s + 4);
   const float y[7] = {y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2]};
+  float D[7];
+  ray_dz(dr, dor, dos, dre, orr, a.o_s[r], D);
+  if (a.dray && s < (size_t)R) store_dray(a.dray, r, D);  // sample k = 0 of each ray
   f32x4 o0, o1;
-  composite_bwd_sample(dr, dor, dos, dre, orr, a.o_s[r], a.weights[s] * a.grad_scale, y, o0, o1);
+  composite_bwd_sample(D, a.weights[s] * a.grad_scale, y, o0, o1);
   *reinterpret_cast<f32x4*>(a.dz4 + 8 * s) = o0;
   *reinterpret_cast<f32x4*>(a.dz4 + 8 * s + 4) = o1;
 }
@@ -764,38 +780,48 @@ extern "C" int mli_ray_batch(const mli_ray_batch_args* a, mli_stream_t s) {
   MLI_LAUNCH_CHECK();
 }
 
-extern "C" int mli_composite_loss(const mli_composite_loss_args* a, mli_stream_t s) {
+// mli_composite_loss geometry, shared by the launch, the finalize and the workspace query: rays
+// per workgroup (two per wave for N <= 128) and workgroups; the partials the finalize sums.
+struct CLGeo {
+  int rpb, nb;
+};
+static CLGeo cl_geo(int R, int N) {
+  const int rpb = N <= 32 * CE ? 2 * CW : CW;
+  return CLGeo{rpb, (R + rpb - 1) / rpb};
+}
+static bool cl_valid(const mli_composite_loss_args* a) {
   const mli_composite_args& c = a->comp;
   const mli_loss_args& l = a->loss;
-  if (c.R <= 0 || c.N <= 0 || c.N > 256 || l.R != c.R || l.N != c.N) return (int)hipErrorInvalidValue;
+  if (c.R <= 0 || c.N <= 0 || c.N > 256 || l.R != c.R || l.N != c.N) return false;
   if (!c.weights || !c.rgb || !c.o_r || !c.o_s || !c.o_re || !a->dz4 || !l.scratch || !l.losses || !l.gt ||
-      !l.outside)
-    return (int)hipErrorInvalidValue;
-  if (l.w_intrinsic != 0.f && (l.sha == nullptr || l.cert == nullptr || l.ref == nullptr))
-    return (int)hipErrorInvalidValue;
-  const int rpb = c.N <= 32 * CE ? 2 * CW : CW;  // rays per block: two per wave for N <= 128
-  const int nb = (c.R + rpb - 1) / rpb;
-  if (rpb == 2 * CW)
-    hipLaunchKernelGGL(composite_loss_kernel<32>, dim3(nb), dim3(CW * 64), 0, (hipStream_t)s, *a);
+      !l.outside || !c.y)
+    return false;
+  return !(l.w_intrinsic != 0.f && (l.sha == nullptr || l.cert == nullptr || l.ref == nullptr));
+}
+
+extern "C" int mli_composite_loss(const mli_composite_loss_args* a, mli_stream_t s) {
+  if (!cl_valid(a)) return (int)hipErrorInvalidValue;
+  const CLGeo g = cl_geo(a->comp.R, a->comp.N);
+  if (g.rpb == 2 * CW)
+    hipLaunchKernelGGL(composite_loss_kernel<32>, dim3(g.nb), dim3(CW * 64), 0, (hipStream_t)s, *a);
   else
-    hipLaunchKernelGGL(composite_loss_kernel<64>, dim3(nb), dim3(CW * 64), 0, (hipStream_t)s, *a);
-  if (!a->defer_finalize) hipLaunchKernelGGL(composite_loss_finalize, dim3(1), dim3(256), 0, (hipStream_t)s, l, nb);
+    hipLaunchKernelGGL(composite_loss_kernel<64>, dim3(g.nb), dim3(CW * 64), 0, (hipStream_t)s, *a);
+  if (!a->defer_finalize)
+    hipLaunchKernelGGL(composite_loss_finalize, dim3(1), dim3(256), 0, (hipStream_t)s, a->loss, g.nb);
   MLI_LAUNCH_CHECK();
 }
 
 extern "C" int mli_composite_loss_finalize(const mli_composite_loss_args* a, mli_stream_t s) {
-  const mli_composite_args& c = a->comp;
-  if (c.R <= 0 || c.N <= 0 || !a->loss.scratch || !a->loss.losses) return (int)hipErrorInvalidValue;
-  const int rpb = c.N <= 32 * CE ? 2 * CW : CW;
-  hipLaunchKernelGGL(composite_loss_finalize, dim3(1), dim3(256), 0, (hipStream_t)s, a->loss, (c.R + rpb - 1) / rpb);
+  if (!cl_valid(a)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(composite_loss_finalize, dim3(1), dim3(256), 0, (hipStream_t)s, a->loss,
+                     cl_geo(a->comp.R, a->comp.N).nb);
   MLI_LAUNCH_CHECK();
 }
 
 extern "C" int mli_composite_loss_workspace(const mli_composite_loss_args* a, int64_t* bytes) {
   const int R = a->comp.R;
   if (R <= 0 || a->comp.N <= 0) return (int)hipErrorInvalidValue;
-  const int rpb = a->comp.N <= 32 * CE ? 2 * CW : CW;
-  bytes[0] = (int64_t)mli_loss::ACC_N * ((R + rpb - 1) / rpb) * 4;  // workgroup partials
+  bytes[0] = (int64_t)mli_loss::ACC_N * cl_geo(R, a->comp.N).nb * 4;  // workgroup partials
   bytes[1] = (int64_t)R * a->comp.N * 8 * 4;                            // dz4
   return 0;
 }

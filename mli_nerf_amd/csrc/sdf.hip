@@ -1014,18 +1014,12 @@ extern "C" int mli_sdf(const mli_sdf_args* a, mli_stream_t s) {
   // 16384 tiles per chunk give FIELD 1.55 / 1.01 / 0.88 / 0.81 / 0.77 ms and steps of 5.49 /
   // 4.90 / 4.60 / 4.53 / 4.66 ms: each chunk pays a launch tail, and one chunk of 640 MiB
   // crowds the heads; 8192 (320 MiB, half of it re-read from the Infinity Cache) is kept.
-#ifndef MLI_FIELD_CHUNK_TILES
-#define MLI_FIELD_CHUNK_TILES 8192
-#endif
-  constexpr int CHUNK_TILES = MLI_FIELD_CHUNK_TILES;
+  constexpr int CHUNK_TILES = 8192;
   for (int t0 = 0; t0 < tiles; t0 += CHUNK_TILES) {
     const int t1 = t0 + CHUNK_TILES < tiles ? t0 + CHUNK_TILES : tiles;
     hipLaunchKernelGGL(encode5_kernel, dim3((t1 - t0 + 3) / 4), dim3(256), 0, (hipStream_t)s, *a, t0, t1);
     int blocks = (t1 - t0 + MLP_WAVES - 1) / MLP_WAVES;
-#ifndef MLI_FIELD_MLP_BLOCKS
-#define MLI_FIELD_MLP_BLOCKS 512
-#endif
-    if (blocks > MLI_FIELD_MLP_BLOCKS) blocks = MLI_FIELD_MLP_BLOCKS;
+    if (blocks > 512) blocks = 512;  // workgroups loop over the chunk's tiles (256 / 1024: DESIGN 9.0)
     hipLaunchKernelGGL(field_mlp_kernel, dim3(blocks), dim3(MLP_WAVES * 64), LDS_SDF, (hipStream_t)s,
                        *a, t0, t1);
     const int e = (int)hipGetLastError();

@@ -378,17 +378,73 @@ __global__ __launch_bounds__(512) void frag_rows_kernel(mli_frag_rows_args a) {
   }
 }
 
+// ---------------------------------------------------------------------- output layer from Q
+// mli_dw4: dW4[c][f] = scale * sum_(wg,seg) dray[ray][3h + c] * q4[wg][seg][h][f][c] (rows f < 256)
+// and db4 from row 256.  Pass 1: workgroup b sums the (wg, seg) items of workgroups
+// [wg0(b), wg0(b+1)) -- one thread per row f (257 rows: thread 0 also takes row 256) -- into
+// ws[b][h][257][4]; pass 2: one workgroup per (h, row) sums the slices in a fixed order.
+constexpr int DW4_SLICES = 256;
+
+__global__ __launch_bounds__(256) void dw4_partial_kernel(mli_dw4_args a) {
+  const int N = a.N, nh = a.n_heads, segs = MLI_Q4_SEGS(N);
+  const int wgs = a.R * N / 256;
+  const int g0 = (int)((int64_t)wgs * blockIdx.x / gridDim.x);
+  const int g1 = (int)((int64_t)wgs * (blockIdx.x + 1) / gridDim.x);
+  const int f = threadIdx.x;
+  f32x4 acc[3], accb[3];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) acc[h] = accb[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int g = g0; g < g1; ++g) {
+    const int r0 = g * 256 / N, nseg = (g * 256 + 255) / N - r0 + 1;
+    for (int sg = 0; sg < nseg; ++sg) {
+      const float* d = a.dray + 8 * (r0 + sg);
+      const f32x4* q = reinterpret_cast<const f32x4*>(a.q4) + ((size_t)g * segs + sg) * nh * 257;
+#pragma unroll
+      for (int h = 0; h < 3; ++h) {
+        if (h >= nh) break;
+        f32x4 dv;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) dv[c] = c < a.k_out[h] ? d[3 * h + c] : 0.f;
+        acc[h] += dv * __builtin_nontemporal_load(q + h * 257 + f);
+        if (f == 0) accb[h] += dv * __builtin_nontemporal_load(q + h * 257 + 256);
+      }
+    }
+  }
+  f32x4* ws = reinterpret_cast<f32x4*>(a.workspace) + (size_t)blockIdx.x * nh * 257;
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    if (h >= nh) break;
+    ws[h * 257 + f] = acc[h];
+    if (f == 0) ws[h * 257 + 256] = accb[h];
+  }
+}
+
+// one workgroup per (h, row): thread j holds slice j (slices <= 256), then a fixed LDS tree
+__global__ __launch_bounds__(256) void dw4_reduce_kernel(mli_dw4_args a, int slices) {
+  __shared__ f32x4 red[256];
+  const int nh = a.n_heads, e = blockIdx.x;  // (h, row)
+  const int h = e / 257, row = e - h * 257, j = threadIdx.x;
+  const f32x4* ws = reinterpret_cast<const f32x4*>(a.workspace);
+  red[j] = j < slices ? ws[(size_t)j * nh * 257 + e] : f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (j < o) red[j] += red[j + o];
+    __syncthreads();
+  }
+  if (j < a.k_out[h]) {
+    const float s = red[0][j] * a.scale;
+    if (row < 256) a.dw[h][j * 256 + row] = s;
+    else a.db[h][j] = s;
+  }
+}
+
 enum { CLS_BIG = 1, CLS_WIDE = 2, CLS_THIN = 4 };
 
-#ifndef MLI_WGRAD_WIDE_SHARE
-#define MLI_WGRAD_WIDE_SHARE 1
-#endif
-constexpr bool WIDE_SHARE = MLI_WGRAD_WIDE_SHARE;
-// WIDE through the LDS-DMA ring (wgrad_dma_kernel) with this many stages; 0: register staging
-#ifndef MLI_WGRAD_WIDE_DMA
-#define MLI_WGRAD_WIDE_DMA 4
-#endif
-constexpr int WIDE_DMA = MLI_WGRAD_WIDE_DMA;
+// WIDE: the three heads' layer-0 jobs share their B rows (x0T) side by side on one XCD
+// (SHARE_B) and stream through the LDS-DMA ring (wgrad_dma_kernel) with this many stages
+// (register staging 0.425 ms, the ring 0.415 ms)
+constexpr bool WIDE_SHARE = true;
+constexpr int WIDE_DMA = 4;
 
 inline int job_class(const mli_wgrad_job& j) {
   return j.M <= 32 ? CLS_THIN : (j.K <= 256 ? CLS_BIG : CLS_WIDE);
@@ -507,4 +563,31 @@ extern "C" int mli_frag_rows(const mli_frag_rows_args* a, mli_stream_t s) {
   if (a->tiles % 8 != 0 || (a->ld % 8) != 0 || (a->col0 % 8) != 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(frag_rows_kernel, dim3(a->tiles / 8), dim3(512), 0, (hipStream_t)s, *a);
   MLI_LAUNCH_CHECK();
+}
+
+static bool dw4_valid(const mli_dw4_args* a) {
+  if (a->R <= 0 || a->N <= 0 || a->N % 32 != 0 || (int64_t)a->R * a->N % 256 != 0 || a->n_heads < 1 ||
+      a->n_heads > 3)
+    return false;
+  for (int h = 0; h < a->n_heads; ++h)
+    if (a->k_out[h] < 1 || a->k_out[h] > 3 || 3 * h + a->k_out[h] > 8) return false;
+  return true;
+}
+
+static int dw4_slices(const mli_dw4_args* a) { return std::min(DW4_SLICES, a->R * a->N / 256); }
+
+extern "C" int mli_dw4(const mli_dw4_args* a, mli_stream_t s) {
+  if (!dw4_valid(a) || !a->q4 || !a->dray || !a->workspace) return (int)hipErrorInvalidValue;
+  for (int h = 0; h < a->n_heads; ++h)
+    if (!a->dw[h] || !a->db[h]) return (int)hipErrorInvalidValue;
+  const int slices = dw4_slices(a);
+  hipLaunchKernelGGL(dw4_partial_kernel, dim3(slices), dim3(256), 0, (hipStream_t)s, *a);
+  hipLaunchKernelGGL(dw4_reduce_kernel, dim3(a->n_heads * 257), dim3(256), 0, (hipStream_t)s, *a, slices);
+  MLI_LAUNCH_CHECK();
+}
+
+extern "C" int mli_dw4_workspace(const mli_dw4_args* a, int64_t* bytes) {
+  if (!dw4_valid(a)) return (int)hipErrorInvalidValue;
+  bytes[0] = (int64_t)dw4_slices(a) * a->n_heads * 257 * 4 * 4;
+  return 0;
 }

@@ -90,15 +90,13 @@ class RenderEngine:
         self.u_fine = (C.c_float * 64)(*(layout.u_fine(cfg.n_fine) + [2.0] * (64 - cfg.n_fine)))
         self._pack_descs = None
         self.trace = None  # set to a list to record per-round sampler outputs (debug/tests)
-        # fixed-order reductions instead of fp32 atomics in mli_wgrad / mli_heads_bwd /
-        # mli_hash_bwd:
+        # fixed-order reductions instead of fp32 atomics in mli_wgrad / mli_hash_bwd:
         # bit-reproducible gradients at the cost of partial-slab traffic
         self.deterministic = False
-        # stage-b heads backward: "fused" = mli_heads_bwd (dX chain + the 256x256 dW in one
-        # launch, dZ_1..3 stay on chip) + the WIDE/THIN dW; "split" = mli_rgb_bwd + mli_wgrad
-        # BIG/WIDE/THIN (dZ_0..3 through HBM)
-        self.heads_bwd = "split"
-        self.heads_split = (0, 0, 0)  # mli_heads_bwd workgroups per (head, layer 1..3); 0 = default
+        # stage-b training: the output layers' dW from per-tile partials the heads forward forms
+        # while X3 is in registers (mli_rgb_fwd PQ mode + mli_dw4) instead of X3 through HBM and
+        # the THIN split-K GEMM; needs N % 32 == 0 (a 32-sample tile within one ray)
+        self.pq = True
         self._wplans = {}   # wgrad plans per buffer set (the prefetch lanes alternate)
         # reference column -> packed k maps of the head layers (constant; uploaded once)
         self._kinv = {(name, li): torch.from_numpy((layout.head_kinv(name, k_in) if li == 0 else
@@ -263,8 +261,25 @@ class RenderEngine:
         self._sdf(rays, dists, N, sdf, mode=1, grad=grad, hess=hess, h0=h0)
         return dict(sdf=sdf, grad=grad, hess=hess, h0=h0, enc=self._bufs["enc5"])
 
+    def pq_mode(self, N, training):
+        """The heads run in PQ mode (mli_rgb_fwd weights / q4, mli_dw4) for this render."""
+        return bool(self.pq and training and self.stage == "b" and N % 32 == 0)
+
     @torch.no_grad()
-    def heads(self, rays, dists, fld, training):
+    def weights(self, rays, dists, fld, s_var, progress):
+        """The composite weights alone (mli_composite_fwd with y = NULL): the PQ heads forward
+        needs them before the heads run (compute_neus_alphas + alpha_compositing_weights,
+        neuralangelo/model.py:492-515, render.py:87-99)."""
+        N, R = dists.shape
+        w = self._buf("weights", (N, R))
+        out = dict(weights=w, rgb=None, o_r=None, o_s=None, o_re=None)
+        L.call("mli_composite_fwd", self._composite_args(rays, dists, fld, dict(y=None), s_var, progress, out))
+        return w
+
+    @torch.no_grad()
+    def heads(self, rays, dists, fld, training, s_var=None, progress=0.0):
+        """Heads forward; stage-b training with ``s_var`` given (and N % 32 == 0) runs the PQ
+        mode: the composite weights first, then the heads with the output-layer partials."""
         N, R = dists.shape
         S = N * R
         nh = len(self.head_specs)
@@ -272,7 +287,8 @@ class RenderEngine:
         if nh == 1:
             y.zero_()  # o_r / o_s slots the single head does not write (composite reads them)
         feat = self._buf("feat", (S * 256,), torch.float16)
-        x0T = xT = masks = None
+        x0T = xT = masks = w = q4 = None
+        pq = s_var is not None and self.pq_mode(N, training)
         if training and self.stage == "b" and not self.deterministic:
             # the split-K dW accumulators of this lane's backward, zeroed here at the start of the
             # step, where the GPU is not shared with the prefetched geometry (before the heads
@@ -281,13 +297,16 @@ class RenderEngine:
             self._bufs["dw_clean"] = True
         if training:
             x0T = self._buf("x0T", (layout.K0, S), torch.float16)
-            xT = self._buf("xT", (nh, 4, 256, S), torch.float16)
+            xT = self._buf("xT", (nh, 3 if pq else 4, 256, S), torch.float16)
             masks = self._buf("masks", (nh, 4, S // 32, 64, 4), torch.int32)
+        if pq:
+            w = self.weights(rays, dists, fld, s_var, progress)
+            q4 = self._buf("q4", (S // 256, layout.q4_segs(N), nh, 257, 4))
         L.call("mli_rgb_fwd", L.RgbFwdArgs(R, N, L.ptr(rays["center"]), L.ptr(rays["ray_unit"]),
                                            L.ptr(rays["pts_light"]), L.ptr(dists), L.ptr(fld["grad"]),
                                            L.ptr(fld["h0"]), L.ptr(self.wfwd), L.ptr(y), L.ptr(feat),
-                                           L.ptr(x0T), L.ptr(xT), L.ptr(masks), nh))
-        return dict(y=y, x0T=x0T, xT=xT, masks=masks, feat=feat)
+                                           L.ptr(x0T), L.ptr(xT), L.ptr(masks), nh, L.ptr(w), L.ptr(q4)))
+        return dict(y=y, x0T=x0T, xT=xT, masks=masks, feat=feat, q4=q4)
 
     @torch.no_grad()
     def composite(self, rays, dists, fld, hd, s_var, progress, training):
@@ -330,12 +349,16 @@ class RenderEngine:
                    rgb=torch.empty(R, 3, device=self.device), o_r=torch.empty(R, 3, device=self.device),
                    o_s=torch.empty(R, 1, device=self.device), o_re=torch.empty(R, 3, device=self.device))
         dz4 = self._buf("dz4", (N, R, 8))
+        dray = self._buf("dray", (R, 8)) if hd.get("q4") is not None else None
         args = L.CompositeLossArgs(self._composite_args(rays, dists, fld, hd, s_var, progress, out), loss,
-                                   self.grad_scale(R), L.ptr(dz4), 1 if defer else 0)
+                                   self.grad_scale(R), L.ptr(dz4), 1 if defer else 0, L.ptr(dray))
         n = L.workspace("mli_composite_loss", args)[0] // 4
         args.loss.scratch = L.ptr(self._buf("cl_scratch", (n,)))
         L.call("mli_composite_loss", args)
         if defer:  # the loss values: finish_losses(), once the gradients are issued
+            if self._bufs.get("cl_deferred") is not None:
+                raise RuntimeError("composite_loss(defer=True): the previous deferred loss values on this "
+                                   "lane were never finished (finish_losses)")
             self._bufs["cl_deferred"] = args
         return out, dz4
 
@@ -344,6 +367,10 @@ class RenderEngine:
         args = self._bufs.pop("cl_deferred", None)
         if args is not None:
             L.call("mli_composite_loss_finalize", args)
+
+    def drop_deferred(self):
+        """Forget a deferred composite_loss whose step failed (its loss slot is not valid)."""
+        self._bufs.pop("cl_deferred", None)
 
     @torch.no_grad()
     def light_visibility(self, rays, comp, iters=20):
@@ -396,7 +423,7 @@ class RenderEngine:
         rays = self.rays(data["pose"], data["intr"], data["pose_light"], data["ray_idx"], W)
         dists = self.sample(rays, u)
         fld = self.field(rays, dists, training)
-        hd = self.heads(rays, dists, fld, training)
+        hd = self.heads(rays, dists, fld, training, s_var, progress)
         if not composite:
             return rays, dists, fld, hd, None
         comp = self.composite(rays, dists, fld, hd, s_var, progress, training)
@@ -415,20 +442,21 @@ class RenderEngine:
     def _dw_total(self):
         return sum(m * k + m for m, k in self._dw_sizes())
 
-    def _wgrad_plan(self, dz_rows, dz4T, hd, dwbuf, flat, grad_out, S):
-        """Split-K jobs (host array) + device assemble descriptors + the fused kernel's dW / db
-        pointers (layers 1..3); cached per buffer set (a few: Trainer.prefetch alternates two
-        engine lanes, each with its own buffers).  dz_rows(hdx, li): the dZ_li rows [256][S]."""
-        key = (dz_rows(0, 0).data_ptr(), dz4T.data_ptr(), hd["x0T"].data_ptr(), hd["xT"].data_ptr(),
-               dwbuf.data_ptr(), flat.data_ptr(), grad_out.data_ptr(), S)
+    def _wgrad_plan(self, dzT, dz4T, hd, dwbuf, flat, grad_out, S):
+        """Split-K jobs (host array) + device assemble descriptors + (PQ mode) the mli_dw4
+        output pointers of the layer-4 dW / db; cached per buffer set (a few: Trainer.prefetch
+        alternates two engine lanes, each with its own buffers)."""
+        pq = hd.get("q4") is not None
+        key = (dzT.data_ptr(), None if dz4T is None else dz4T.data_ptr(), hd["x0T"].data_ptr(),
+               hd["xT"].data_ptr(), dwbuf.data_ptr(), flat.data_ptr(), grad_out.data_ptr(), S, pq)
         hit = self._wplans.get(key)
         if hit is not None:
-            return hit[0], hit[1], hit[2]
+            return hit
         if len(self._wplans) >= 8:
             self._wplans.clear()
         sizes = self._dw_sizes()
         jobs, assemble, off = [], [], 0
-        fused_dw, fused_db = [0] * 9, [0] * 9
+        dw4, db4, k4 = [None] * 3, [None] * 3, [0] * 3
         for hdx, (name, k_in, k_out) in enumerate(layout.HEADS):
             for li in range(5):
                 m, k = sizes[hdx * 5 + li]
@@ -436,13 +464,14 @@ class RenderEngine:
                 db = dwbuf[off + m * k:off + m * k + m]
                 off += m * k + m
                 if li == 0:
-                    a_rows, b_rows = dz_rows(hdx, 0), hd["x0T"]
+                    jobs.append(L.WgradJob(L.ptr(dzT[hdx, 0]), L.ptr(hd["x0T"]), m, k, L.ptr(dw), L.ptr(db), k))
                 elif li < 4:
-                    a_rows, b_rows = dz_rows(hdx, li), hd["xT"][hdx, li - 1]
-                    fused_dw[hdx * 3 + li - 1], fused_db[hdx * 3 + li - 1] = L.ptr(dw), L.ptr(db)
+                    jobs.append(L.WgradJob(L.ptr(dzT[hdx, li]), L.ptr(hd["xT"][hdx, li - 1]), m, k, L.ptr(dw),
+                                           L.ptr(db), k))
+                elif pq:
+                    dw4[hdx], db4[hdx], k4[hdx] = L.ptr(dw), L.ptr(db), m
                 else:
-                    a_rows, b_rows = dz4T[hdx], hd["xT"][hdx, 3]
-                jobs.append(L.WgradJob(L.ptr(a_rows), L.ptr(b_rows), m, k, L.ptr(dw), L.ptr(db), k))
+                    jobs.append(L.WgradJob(L.ptr(dz4T[hdx]), L.ptr(hd["xT"][hdx, 3]), m, k, L.ptr(dw), L.ptr(db), k))
                 pre = layout.param_prefix(name, li)
                 v = self.param_view(flat, pre + ".weight_v")
                 g = self.param_view(flat, pre + ".weight_g")
@@ -454,9 +483,9 @@ class RenderEngine:
                                                 L.ptr(self.param_view(grad_out, pre + ".bias")), None))
         job_arr = (L.WgradJob * len(jobs))(*jobs)
         ad = _to_device_structs(assemble, self.device)
-        ptrs = ((C.c_void_p * 9)(*fused_dw), (C.c_void_p * 9)(*fused_db))
-        self._wplans[key] = (job_arr, ad, ptrs)
-        return job_arr, ad, ptrs
+        plan = (job_arr, ad, (dw4, db4, k4))
+        self._wplans[key] = plan
+        return plan
 
     def _wgrad(self, S, jobs, classes):
         """mli_wgrad over `classes` (separate launches, timed separately); deterministic mode:
@@ -475,46 +504,39 @@ class RenderEngine:
     def backward(self, st, d_rgb, d_o_r, d_o_s, d_o_re, flat, sdf_l1, grad_out, dz4=None):
         """Gradient of the loss w.r.t. the trainable head parameters into grad_out (flat), from
         d loss / d (rgb, o_r, o_s, o_re) -- or from ``dz4`` when composite_loss already ran the
-        composite backward (the d_* are then unused)."""
+        composite backward (the d_* are then unused; in PQ mode it also wrote the per-ray D)."""
         rays, dists, fld, hd, comp = st
         N, R = dists.shape
         S = N * R
         scale = self.grad_scale(R)
+        pq = hd.get("q4") is not None
         if dz4 is None:
             dz4 = self._buf("dz4", (N, R, 8))
             c = lambda t: None if t is None else t.contiguous()  # noqa: E731
             L.call("mli_composite_bwd", L.CompositeBwdArgs(R, N, L.ptr(comp["weights"]), L.ptr(hd["y"]),
                                                            L.ptr(comp["o_r"]), L.ptr(comp["o_s"]), L.ptr(c(d_rgb)),
                                                            L.ptr(c(d_o_r)), L.ptr(c(d_o_s)), L.ptr(c(d_o_re)),
-                                                           scale, L.ptr(dz4)))
-        dz4T = self._buf("dz4T", (3, 4, S), torch.float16)
+                                                           scale, L.ptr(dz4),
+                                                           L.ptr(self._buf("dray", (R, 8)) if pq else None)))
+        dz4T = None if pq else self._buf("dz4T", (3, 4, S), torch.float16)
         dwbuf = self._buf("dw", (self._dw_total(),))
         if not self.deterministic and not self._bufs.pop("dw_clean", False):
             dwbuf.zero_()  # split-K partials add into it (fp32 atomics); heads() zeroes it once per render
-        if self.heads_bwd == "fused":
-            # dX chain + dW of the 256x256 layers in one launch; it writes dZ_0 and dz4 rows for
-            # the layer-0 (WIDE) and layer-4 (THIN) dW
-            dz0T = self._buf("dz0T", (3, 256, S), torch.float16)
-            dz1f = self._buf("dz1f", (3 * 256 * S,), torch.float16)  # dZ_1 fragments (second launch)
-            jobs, ad, (pdw, pdb) = self._wgrad_plan(lambda h, li: dz0T[h], dz4T, hd, dwbuf, flat, grad_out, S)
-            args = L.HeadsBwdArgs(R, N, L.ptr(dz4), L.ptr(self.wbwd), L.ptr(hd["masks"]), L.ptr(hd["xT"]),
-                                  L.ptr(dz0T), L.ptr(dz4T), L.ptr(dz1f), pdw, pdb,
-                                  (C.c_int * 3)(*self.heads_split), 1 if self.deterministic else 0, None)
-            if self.deterministic:
-                nbytes = L.workspace("mli_heads_bwd", args)[2]
-                args.workspace = L.ptr(self._buf("heads_ws", (max(nbytes, 4) // 4,)))
-            L.call("mli_heads_bwd", args)
-            classes = (2, 4)  # WIDE, THIN
-        else:
-            dzT = self._buf("dzT", (3, 4, 256, S), torch.float16)
-            L.call("mli_rgb_bwd", L.RgbBwdArgs(R, N, L.ptr(dz4), L.ptr(self.wbwd), L.ptr(hd["masks"]), L.ptr(dzT),
-                                               L.ptr(dz4T)))
-            jobs, ad, _ = self._wgrad_plan(lambda h, li: dzT[h, li], dz4T, hd, dwbuf, flat, grad_out, S)
-            classes = (1, 2, 4)  # BIG, WIDE, THIN launch classes
+        dzT = self._buf("dzT", (3, 4, 256, S), torch.float16)
+        L.call("mli_rgb_bwd", L.RgbBwdArgs(R, N, L.ptr(dz4), L.ptr(self.wbwd), L.ptr(hd["masks"]), L.ptr(dzT),
+                                           L.ptr(dz4T)))
+        jobs, ad, (dw4, db4, k4) = self._wgrad_plan(dzT, dz4T, hd, dwbuf, flat, grad_out, S)
         if self.gate_wgrad:  # Trainer.prefetch(gate="wgrad"): next geometry may start here
             self.gate_event = torch.cuda.Event()
             self.gate_event.record()
-        self._wgrad(S, jobs, classes)
+        if pq:
+            args = L.Dw4Args(R, N, 3, L.ptr(hd["q4"]), L.ptr(self._bufs["dray"]), scale / L.Q4_SCALE,
+                             (C.c_void_p * 3)(*dw4), (C.c_void_p * 3)(*db4), (C.c_int * 3)(*k4), None)
+            args.workspace = L.ptr(self._buf("dw4_ws", (L.workspace("mli_dw4", args)[0] // 4,)))
+            L.call("mli_dw4", args)
+            self._wgrad(S, jobs, (1, 2))  # BIG, WIDE
+        else:
+            self._wgrad(S, jobs, (1, 2, 4))  # BIG, WIDE, THIN launch classes
         L.call("mli_grad_assemble", L.AssembleArgs(15, L.ptr(ad), 1.0 / scale))
         return grad_out
 

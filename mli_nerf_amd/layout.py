@@ -158,3 +158,10 @@ def u_fine(n_fine):
 
 def fastmod_magic(d):
     return ((1 << 64) // d + 1) & ((1 << 64) - 1)
+
+
+def q4_segs(N):
+    """MLI_Q4_SEGS (include/mli_hip.h): ray segments per 256-sample workgroup of the PQ partials."""
+    if 256 % N == 0:
+        return 256 // N
+    return 1 if N % 256 == 0 else 256 // N + 2

@@ -253,8 +253,7 @@ class Model(torch.nn.Module):
         self._sdf_version = None
         self.image_width = self.image_size_train[1]
         self.deterministic = False  # fixed-order gradient reductions (RenderEngine.deterministic)
-        self.heads_bwd = "split"    # stage-b heads backward kernels (RenderEngine.heads_bwd)
-        self.heads_split = (0, 0, 0)
+        self.pq = True              # stage-b output-layer dW from the forward's partials (RenderEngine.pq)
 
     # -------------------------------------------------------------- parameter plumbing
     def _view(self, name, flat=None):
@@ -376,7 +375,7 @@ class Model(torch.nn.Module):
         sdf = self.neural_sdf
         eng = self.engine
         eng.deterministic = self.deterministic
-        eng.heads_bwd, eng.heads_split = self.heads_bwd, tuple(self.heads_split)
+        eng.pq = self.pq
         eng.set_normal_eps(sdf.normal_eps)
         eng.active_levels = int(sdf.active_levels)
         l0 = sdf.mlp.linears[0]

@@ -147,6 +147,67 @@ def reduce_gradients(grad, world_size, group=None):
     return grad
 
 
+class Checkpointer:
+    """imaginaire/trainers/base.py:557-687 surface over the Trainer's checkpoint layout:
+    ``trainer.checkpointer.load(path, resume, load_opt=..., load_sch=...)`` as test.py:93 calls
+    it, ``save(epoch, iteration, latest)``, the ``latest_checkpoint.txt`` pointer in cfg.logdir."""
+
+    def __init__(self, cfg, trainer):
+        self.trainer = trainer
+        self.logdir = cfg.get("logdir", None)
+        ck = cfg.get("checkpoint", None) or {}
+        self.strict_resume = bool(ck.get("strict_resume", True))
+        self.resume = False
+        self.resume_epoch = self.resume_iteration = None
+        self.eval_epoch = self.eval_iteration = None
+        self.checkpoint_path = None
+
+    def _get_full_path(self, name):
+        return os.path.join(self.logdir or ".", name)
+
+    def read_latest_checkpoint_file(self):
+        """base.py:663-671 (incl. the old 'latest_checkpoint: <file>' form)."""
+        path = self._get_full_path("latest_checkpoint.txt")
+        if not os.path.exists(path):
+            return None
+        name = open(path).read().strip()
+        return name.split(" ")[-1] if name.startswith("latest_checkpoint:") else name
+
+    def load(self, checkpoint_path=None, resume=False, load_opt=True, load_sch=True, **kwargs):
+        """base.py:609-652: priority (1) checkpoint_path, (2) with ``resume`` the latest checkpoint of
+        cfg.logdir, (3) nothing (train from scratch).  Model weights with cfg.checkpoint.strict_resume;
+        with ``resume`` also epoch / iteration and (optionally) the optimizer / scheduler."""
+        self.resume = resume
+        if resume and checkpoint_path is None:
+            latest = self.read_latest_checkpoint_file()
+            if latest is not None:
+                checkpoint_path = self._get_full_path(latest)
+        if checkpoint_path is None:
+            return None
+        if not os.path.exists(checkpoint_path):
+            raise FileNotFoundError("File not found (local): %s" % checkpoint_path)
+        self.checkpoint_path = checkpoint_path
+        tr = self.trainer
+        res = tr.load_checkpoint(checkpoint_path, resume=resume, strict=self.strict_resume,
+                                 load_opt=load_opt and tr.optim is not None, load_sch=load_sch)
+        meta = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
+        self.eval_epoch, self.eval_iteration = meta.get("epoch"), meta.get("iteration")
+        if resume:
+            self.resume_epoch, self.resume_iteration = self.eval_epoch, self.eval_iteration
+        return res
+
+    def save(self, current_epoch, current_iteration, latest=False):
+        """base.py:569-589 (synchronously; master only under a process group)."""
+        import torch.distributed as dist
+        tr = self.trainer
+        tr.current_epoch, tr.current_iteration = current_epoch, current_iteration
+        if dist.is_available() and dist.is_initialized() and dist.get_rank() != 0:
+            name = "latest_checkpoint.pt" if latest else \
+                "epoch_{:05}_iteration_{:09}_checkpoint.pt".format(current_epoch, current_iteration)
+            return self._get_full_path(name)
+        return tr.save_checkpoint(self.logdir or ".", latest=latest)
+
+
 class Trainer:
     """Stage-b / stage-a trainer: ``train_step(data)`` = forward + loss + backward + AdamW."""
 
@@ -210,6 +271,7 @@ class Trainer:
         self.current_iteration = 0
         self.current_epoch = 0
         self.losses, self.metrics = {}, {}
+        self.checkpointer = Checkpointer(cfg, self)
 
     # ------------------------------------------------------------ construction (reference)
     @staticmethod
@@ -399,7 +461,7 @@ class Trainer:
             lane, rays, dists, fld, done = pf
             torch.cuda.current_stream(m.flat.device).wait_event(done)
             eng.use_lane(lane)
-            hd = eng.heads(rays, dists, fld, True)
+            hd = eng.heads(rays, dists, fld, True, m.s_var.detach(), m.progress)
             comp = None if fused else eng.composite(rays, dists, fld, hd, m.s_var.detach(), m.progress, True)
             st = (rays, dists, fld, hd, comp)
         if self.prefetch_gate == "heads":
@@ -415,7 +477,11 @@ class Trainer:
             comp, dz4 = eng.composite_loss(rays, dists, fld, hd, m.s_var.detach(), m.progress,
                                            self._loss_args(rays, fld, None, data, lv), defer=True)
             st = (rays, dists, fld, hd, comp)
-            eng.backward(st, None, None, None, None, m.flat, m._sdf_l1(), grad, dz4=dz4)
+            try:
+                eng.backward(st, None, None, None, None, m.flat, m._sdf_l1(), grad, dz4=dz4)
+            except BaseException:
+                eng.drop_deferred()
+                raise
             eng.finish_losses()
         else:
             d_rgb, d_o_r, d_o_s, d_o_re = self._fused_losses(st, data, lv)
@@ -669,9 +735,19 @@ class Trainer:
             self.optim_table.resize(self.model.neural_sdf.tcnn_encoding.params.numel())
         return res
 
-    def test_video(self, dataset, setting1, setting2, output_dir, mode="test",
+    def test_video(self, data_loader, setting1, setting2, output_dir, mode="test",
                    video_content=("rgb", "gt", "o_r", "o_s"), show_pbar=False):
-        """projects/nerf/trainers/base.py:264-346 (see mli_nerf_amd.video)."""
+        """projects/nerf/trainers/base.py:264-346 (see mli_nerf_amd.video); ``data_loader`` as
+        test.py:142 passes it (its ``.dataset`` is used) or the Dataset itself."""
         from . import video
+        dataset = getattr(data_loader, "dataset", data_loader)
         return video.render_video(self.model, dataset, setting1, setting2, output_dir, trainer=self, mode=mode,
                                   video_content=video_content, show_pbar=show_pbar)
+
+    def test_all_light(self, data_loader, output_dir=None, mode="test", dataset_type="pair", sample_num=4,
+                       seed=999):
+        """NeuralLumen/trainer.py:216-316: every (camera, light) pair of the enumeration
+        (pair / unpair / limitedlights) rendered with the light-visibility pass, the maps saved as
+        PNGs and ``results_all.pt`` for scripts/pseudo_label.py (see mli_nerf_amd.relight)."""
+        from . import relight
+        return relight.test_all_light(self, data_loader, output_dir, mode, dataset_type, sample_num, seed)

@@ -26,7 +26,7 @@ STRUCTS = {
     "mli_composite_bwd_geo_args": L.CompositeBwdGeoArgs, "mli_geo_bwd_args": L.GeoBwdArgs,
     "mli_sdf_bwd_args": L.SdfBwdArgs, "mli_pack_sdf_t_args": L.PackSdfTArgs, "mli_hash_bwd_args": L.HashBwdArgs,
     "mli_frag_rows_args": L.FragRowsArgs, "mli_light_visibility_args": L.LightVisibilityArgs,
-    "mli_ray_batch_args": L.RayBatchArgs, "mli_heads_bwd_args": L.HeadsBwdArgs,
+    "mli_ray_batch_args": L.RayBatchArgs, "mli_dw4_args": L.Dw4Args,
     "mli_composite_loss_args": L.CompositeLossArgs,
 }
 
@@ -97,7 +97,23 @@ def test_workspace_queries_match_engine_buffers():
     assert L.workspace("mli_sdf", L.SdfArgs(1, R, N)) == [(S // 32) * 32 * 640 * f16]
     assert L.workspace("mli_sdf", L.SdfArgs(0, R, 64)) == [0]
     assert L.workspace("mli_rgb_fwd", L.RgbFwdArgs(R, N, n_heads=3)) == [
-        N * R * 8 * f32, S * 256 * f16, layout.K0 * S * f16, 3 * 4 * 256 * S * f16, 3 * 4 * (S // 32) * 64 * 4 * 4]
+        N * R * 8 * f32, S * 256 * f16, layout.K0 * S * f16, 3 * 4 * 256 * S * f16, 3 * 4 * (S // 32) * 64 * 4 * 4, 0]
+    # PQ mode (weights set): X3 not stored, the output-layer partials q4 instead
+    pq = L.RgbFwdArgs(R, N, n_heads=3)
+    pq.weights = 1
+    assert L.workspace("mli_rgb_fwd", pq)[3:] == [3 * 3 * 256 * S * f16, 3 * 4 * (S // 32) * 64 * 4 * 4,
+                                                  (S // 256) * 2 * 3 * 257 * 4 * f32]   # 2 rays per workgroup
+    assert [layout.q4_segs(n) for n in (32, 64, 96, 128, 192, 256, 384, 512)] == [8, 4, 4, 2, 3, 1, 2, 1]
+    pq.N = 96 + 8   # a 32-sample tile would straddle two rays
+    pq.R = 256
+    with pytest.raises(RuntimeError):
+        L.workspace("mli_rgb_fwd", pq)
+    d4 = L.Dw4Args(R, N, 3)
+    d4.k_out = (C.c_int * 3)(3, 3, 1)
+    assert L.workspace("mli_dw4", d4) == [256 * 3 * 257 * 4 * f32]
+    d4.k_out = (C.c_int * 3)(3, 3, 4)   # head 2 has one output slot left in dray
+    with pytest.raises(RuntimeError):
+        L.workspace("mli_dw4", d4)
     assert L.workspace("mli_rgb_bwd", L.RgbBwdArgs(R, N)) == [3 * 4 * 256 * S * f16, 3 * 4 * S * f16]
     assert L.workspace("mli_geo_bwd", L.GeoBwdArgs(R, N)) == [
         4 * 256 * S * f16, 4 * S * f16, N * R * 4 * f32, 256 * S * f16, S * 256 * f16, 0]
@@ -112,15 +128,6 @@ def test_workspace_queries_match_engine_buffers():
     n_params = 45724048 * 8
     assert L.workspace("mli_hash_bwd", L.HashBwdArgs(R, N, deterministic=1, n_params=n_params)) == [n_params * 8]
     assert L.workspace("mli_hash_bwd", L.HashBwdArgs(R, N, n_params=n_params)) == [0]
-    # fused heads backward: dZ_0 rows, dz4 rows; deterministic slabs of the 9 (head, layer) dW + db
-    assert L.workspace("mli_heads_bwd", L.HeadsBwdArgs(R, N)) == [3 * 256 * S * f16, 3 * 4 * S * f16, 0,
-                                                                   3 * 256 * S * f16]
-    hb = L.HeadsBwdArgs(R, N, deterministic=1)
-    assert L.workspace("mli_heads_bwd", hb)[2] == 3 * (48 + 24 + 12) * (256 * 256 + 256) * f32
-    hb.split = (C.c_int * 3)(8, 4, 2)
-    assert L.workspace("mli_heads_bwd", hb)[2] == 3 * (8 + 4 + 2) * (256 * 256 + 256) * f32
-    with pytest.raises(RuntimeError):
-        L.workspace("mli_heads_bwd", L.HeadsBwdArgs(128, 1))   # S not a multiple of 256
     # wgrad: the stage-b jobs (engine._wgrad_plan shapes): partial slabs only in deterministic mode
     jobs = []
     for name, k_in, k_out in layout.HEADS:

@@ -91,3 +91,34 @@ def test_prefetch_is_a_no_op_outside_the_fused_stage_b_path():
     trb.weights["unfused_term"] = 1.0
     trb.prefetch(batch)
     assert trb._pending == []
+
+
+def test_checkpointer_adapter_as_test_py_calls_it(tmp_path):
+    """trainer.checkpointer.load(args.checkpoint, args.resume, load_sch=False, load_opt=False)
+    (test.py:93 over imaginaire/trainers/base.py:609-652): an explicit path loads the model only
+    (resume False) or the metadata too (resume True); resume with no path takes cfg.logdir's
+    latest_checkpoint.txt; no path and no resume trains from scratch; a missing file raises."""
+    import pytest
+    from mli_nerf_amd.trainer import Trainer
+    cfg, m = _model("b")
+    cfg["logdir"] = str(tmp_path)
+    tr = Trainer(cfg, is_inference=False, model=m)
+    path = tr.checkpointer.save(3, 777)
+    assert os.path.basename(path) == "epoch_00003_iteration_000000777_checkpoint.pt"
+    assert (tmp_path / "latest_checkpoint.txt").read_text().strip() == os.path.basename(path)
+    cfg2, m2 = _model("b", seed=1)
+    cfg2["logdir"] = str(tmp_path)
+    tr2 = Trainer(cfg2, is_inference=True, model=m2)
+    assert tr2.checkpointer.load(None, False) is None          # from scratch
+    tr2.checkpointer.load(path, False, load_sch=False, load_opt=False)
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, m2.state_dict()[k]), k
+    assert tr2.current_iteration == 0 and tr2.checkpointer.eval_iteration == 777
+    cfg3, m3 = _model("b", seed=2)
+    cfg3["logdir"] = str(tmp_path)
+    tr3 = Trainer(cfg3, is_inference=False, model=m3)
+    tr3.checkpointer.load(None, True)                          # latest of cfg.logdir
+    assert tr3.current_iteration == 777 and tr3.current_epoch == 3 and tr3.checkpointer.resume_iteration == 777
+    assert torch.equal(m3.s_var, m.s_var)
+    with pytest.raises(FileNotFoundError):
+        tr3.checkpointer.load(str(tmp_path / "nope.pt"), False)
