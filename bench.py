@@ -161,16 +161,16 @@ def run_infer(args, world, rank, dev):
 
     for f in range(args.warmup):
         model.inference(frames[f])
-    torch.cuda.synchronize()
+    PLATFORM.sync()
     barrier()
-    torch.cuda.synchronize()
+    PLATFORM.sync()
     t0 = time.perf_counter()
     out = None
     for f in range(args.warmup, args.warmup + args.frames):
         out = model.inference(frames[f])
-    torch.cuda.synchronize()
+    PLATFORM.sync()
     barrier()
-    torch.cuda.synchronize()
+    PLATFORM.sync()
     elapsed = time.perf_counter() - t0
     # per-kernel HIP events over one more (untimed) frame rendered with the chunk pipeline off:
     # with two chunks in flight an event pair would also time the other stream's kernels
@@ -305,6 +305,68 @@ def cpu_baseline(cfg, R_cpu, steps, threads, stage_a=None):
                 s_per_step=t), data, u, float(psnr)
 
 
+def count_gpus():
+    """GPUs this process may use, counted WITHOUT initialising HIP: the KFD topology nodes that
+    have SIMDs (sysfs), narrowed by ROCR/HIP/CUDA_VISIBLE_DEVICES.  The parent of ``--gpus N``
+    spawns the ranks and must never open the GPU itself (a process that initialised HIP must not
+    start others by fork / exec)."""
+    import re
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    for d in (sorted(os.listdir(base)) if os.path.isdir(base) else []):
+        try:
+            with open(os.path.join(base, d, "properties")) as f:
+                props = f.read()
+        except OSError:
+            continue
+        m = re.search(r"^simd_count\s+(\d+)", props, re.M)
+        if m and int(m.group(1)) > 0:
+            n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
+def gpu_handles():
+    """This process's open GPU device files (/dev/kfd, /dev/dri/*): empty while HIP is untouched."""
+    out = []
+    fd_dir = "/proc/self/fd"
+    for fd in (os.listdir(fd_dir) if os.path.isdir(fd_dir) else []):
+        try:
+            tgt = os.readlink(os.path.join(fd_dir, fd))
+        except OSError:
+            continue
+        if tgt == "/dev/kfd" or tgt.startswith("/dev/dri/"):
+            out.append(tgt)
+    return out
+
+
+class HipPlatform:
+    """A rank's device plumbing: its GPU, stream sync, the collective backend.
+    tests/test_bench_launch.py swaps in a CPU stand-in (with tests/stub_engine.py) to rehearse the
+    --gpus N process flow end to end on CPU; the bench itself always runs this one."""
+    name = "hip"
+
+    def device(self, local):
+        torch.cuda.set_device(local)
+        return torch.device("cuda", local)
+
+    def sync(self):
+        torch.cuda.synchronize()
+
+    def priority_range(self):
+        return torch.cuda.Stream.priority_range()
+
+    def backend(self, rehearse):
+        return "gloo" if rehearse else "nccl"
+
+
+PLATFORM = HipPlatform()
+WORKER_SCRIPT = None   # the rank program --gpus N spawns (default: this file)
+
+
 def _free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -321,6 +383,10 @@ def launch_workers(n, argv, script=None, poll_s=0.2):
     code, else 0."""
     import subprocess
     script = script or os.path.abspath(__file__)
+    held = gpu_handles()
+    if held:
+        raise RuntimeError("launch_workers: this process holds GPU device files %s; the ranks must be "
+                           "started by a process that never initialised HIP" % held)
     port = _free_port()
     procs = []
     for r in range(n):
@@ -351,7 +417,8 @@ def launch_workers(n, argv, script=None, poll_s=0.2):
     return rc or next((p.returncode for p in procs if p.returncode), 0)
 
 
-def main():
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
                     help="GPUs of this node; without a launcher's WORLD_SIZE, one process per GPU is spawned")
@@ -390,12 +457,12 @@ def main():
     ap.add_argument("--iteration", type=int, default=100000,
                     help="stage a (--config syn_hotdog_a): training iteration (sets the coarse-to-fine "
                          "levels, tap epsilon and curvature weight; >= 80000: all 16 levels active)")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        n_dev = torch.cuda.device_count()  # counts without initialising the GPU
+        n_dev = count_gpus()  # sysfs: HIP stays uninitialised in this process
         if n_dev < args.gpus:
             raise SystemExit("--gpus %d: only %d GPU(s) visible" % (args.gpus, n_dev))
-        sys.exit(launch_workers(args.gpus, sys.argv[1:]))
+        sys.exit(launch_workers(args.gpus, argv, script=WORKER_SCRIPT))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -405,15 +472,15 @@ def main():
     rehearse = os.environ.get("MLI_BENCH_REHEARSE") == "1"
     if rehearse:
         local = 0
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    dev = PLATFORM.device(local)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if rehearse:
-            dist.init_process_group("gloo")
-        else:
+        backend = PLATFORM.backend(rehearse)
+        if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from mli_nerf_amd import _lib as L, synthetic
     from mli_nerf_amd.configs import preset
@@ -441,7 +508,13 @@ def main():
     n_frames = 8
     g = torch.Generator().manual_seed(1000 + rank)
     cams = []
-    for f in range(n_frames):
+    real_cams = args.config == "rene_savannah_b"
+    if real_cams:
+        # configs[3]: the reference's real ReNe savannah camera + light poses, rank r -> frame r
+        # (dataset_rene/savannah/train_transforms.json, committed as tests/golden/rene_savannah_train16.json)
+        from mli_nerf_amd.data import rene_savannah_cameras
+        cams = [rene_savannah_cameras(Hh, W, frames=[rank % 16])[0]] * n_frames
+    for f in range(0 if real_cams else n_frames):
         fb = synthetic.make_batch(1, H=Hh, W=W, frame=rank * n_frames + f)
         cams.append((fb["intr"][0], fb["pose"][0], fb["pose_light"][0]))
     feed = DeviceFeed(device=dev, images=torch.rand(n_frames, 3, Hh * W, generator=g),
@@ -462,7 +535,7 @@ def main():
     # frozen SDF) on a side stream (Trainer.prefetch), and trains on batch k.  Every timed step
     # still draws, samples, renders and trains one full batch.  On by default (gate heads).
     # stream priorities (experiment): torch range (lowest, highest)
-    lo, hi = torch.cuda.Stream.priority_range()
+    lo, hi = PLATFORM.priority_range()
     if args.priority == "side":
         trainer.side_priority = hi
     main_stream = torch.cuda.Stream(device=dev, priority=hi) if args.priority == "main" else None
@@ -488,10 +561,10 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    PLATFORM.sync()
     progress("warm-up done (%d steps)" % args.warmup)
     barrier()
-    torch.cuda.synchronize()
+    PLATFORM.sync()
     names = None if args.time_all_kernels else {"mli_rgb_fwd", "mli_rgb_bwd", "mli_dw4", "mli_wgrad", "mli_sdf"}
     if not args.no_kernel_timing and not pipe:
         L.PROFILE = []  # per-kernel HIP events on the launch stream, over the timed region
@@ -499,9 +572,9 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    PLATFORM.sync()
     barrier()
-    torch.cuda.synchronize()
+    PLATFORM.sync()
     elapsed = time.perf_counter() - t0
     progress("timed steps done: %.3f ms/step" % (elapsed / args.steps * 1e3))
     prof, L.PROFILE = L.PROFILE, None
@@ -534,7 +607,9 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp16",
         "dtype_detail": "fp16 MFMA operands, fp32 accumulate; fp32 sampling / compositing / losses / AdamW",
-        "data": "synthetic (seeded cameras/lights/labels, random-init weights, full 2^22 hash table)",
+        "data": ("real ReNe savannah cameras/lights (frame = rank), synthetic images/labels, random-init "
+                 "weights, full 2^22 hash table" if real_cams else
+                 "synthetic (seeded cameras/lights/labels, random-init weights, full 2^22 hash table)"),
         "config": {"workload": "%s stage-%s train step" % (args.config, model.stage), "rays_per_gpu": R,
                    "samples_per_ray": N, "global_rays": R * world, "image": [Hh, W], "parallelism": "dp%d" % world,
                    "pipeline": ("geometry prefetch on a side stream, gate " + args.pipeline) if pipe else "off",

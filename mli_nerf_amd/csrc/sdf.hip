@@ -21,6 +21,8 @@
 // head.  Chunks keep the encodings Infinity-Cache resident between the two.
 #include "hashgrid.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int SDF_WAVES = 4;
@@ -139,9 +141,10 @@ MLI_FI float sdf_point(const uint8_t* lds, const uint16_t* __restrict__ table, c
 // hash_level (bit-identical encodings), written as B-fragment images for phase B.
 constexpr int TAPS = 5;
 
-template <int KIND>
+// sink(p, e): the fp16 encoding e (8 features of this lane's level) of point p
+template <int KIND, class Sink>
 MLI_FI void level5(const uint16_t* __restrict__ table, const LevelP& P, const float (&x)[TAPS][3], bool keep,
-                   uint16_t* __restrict__ dst /* enc + (tile*5*8 + q)*512 + lane*8 */) {
+                   Sink&& sink) {
   const uint32_t r2 = P.res * P.res;
   const bool dense_lane = (uint64_t)P.res * P.res * P.res <= (uint64_t)P.size;
   auto index_of = [&](uint32_t cx, uint32_t cy, uint32_t cz, bool skip_mod) MLI_LAMBDA_FI {
@@ -160,7 +163,7 @@ MLI_FI void level5(const uint16_t* __restrict__ table, const LevelP& P, const fl
       pos[d] = p - fl;
     }
   };
-  auto interp_store = [&](const u32x4 (&cv)[8], const float (&pos)[3], uint16_t* out) MLI_LAMBDA_FI {
+  auto interp_store = [&](const u32x4 (&cv)[8], const float (&pos)[3], int pt) MLI_LAMBDA_FI {
     float acc[8];
 #pragma unroll
     for (int f = 0; f < 8; ++f) acc[f] = 0.0f;
@@ -181,7 +184,7 @@ MLI_FI void level5(const uint16_t* __restrict__ table, const LevelP& P, const fl
     half8 e;
 #pragma unroll
     for (int f = 0; f < 8; ++f) e[f] = (f16)(keep ? acc[f] : 0.0f);  // c2f mask
-    *reinterpret_cast<half8*>(out) = e;
+    sink(pt, e);
   };
   // center
   uint32_t g0[3];
@@ -195,7 +198,7 @@ MLI_FI void level5(const uint16_t* __restrict__ table, const LevelP& P, const fl
     const uint32_t idx = index_of(g0[0] + (c & 1), g0[1] + ((c >> 1) & 1), g0[2] + ((c >> 2) & 1), skip_mod);
     cc[c] = *reinterpret_cast<const u32x4*>(table + (size_t)(P.offset + idx) * 8);
   }
-  interp_store(cc, pos0, dst);
+  interp_store(cc, pos0, 0);
   // taps
 #pragma unroll
   for (int p = 1; p < TAPS; ++p) {
@@ -213,7 +216,7 @@ MLI_FI void level5(const uint16_t* __restrict__ table, const LevelP& P, const fl
         tc[c] = *reinterpret_cast<const u32x4*>(table + (size_t)(P.offset + idx) * 8);
       }
     }
-    interp_store(tc, pos, dst + (size_t)p * 8 * 512);
+    interp_store(tc, pos, p);
   }
 }
 
@@ -268,12 +271,15 @@ __global__ __launch_bounds__(256) void encode5_kernel(mli_sdf_args a, int tile0,
       continue;
     }
     const bool keep = (h ? lv1 : lv0) < a.active_levels;
+    auto sink = [&](int p, const half8& e) MLI_LAMBDA_FI {
+      *reinterpret_cast<half8*>(dst + (size_t)p * 8 * 512) = e;
+    };
     if (d0 && d1)
-      level5<0>(a.table, P, x, keep, dst);
+      level5<0>(a.table, P, x, keep, sink);
     else if (!d0 && !d1)
-      level5<1>(a.table, P, x, keep, dst);
+      level5<1>(a.table, P, x, keep, sink);
     else
-      level5<2>(a.table, P, x, keep, dst);
+      level5<2>(a.table, P, x, keep, sink);
   }
 }
 
@@ -316,6 +322,150 @@ __global__ __launch_bounds__(MLP_WAVES * 64) void field_mlp_kernel(mli_sdf_args 
 #pragma unroll
       for (int j = 0; j < TAPS; ++j) s[j] = pi == j ? v : s[j];
     }
+    float s0 = s[0];
+    const float s1 = s[1], s2 = s[2], s3 = s[3], s4 = s[4];
+    if (a.outside[r]) s0 = a.outside_val;
+    if (valid && h == 0) {
+      a.sdf[slot] = s0;
+      // (k1*s1 + k2*s2 + k3*s3 + k4*s4) / (4 eps), summed left to right per component.
+      const float gx = __fadd_rn(__fadd_rn(__fadd_rn(s1, -s2), -s3), s4);
+      const float gy = __fadd_rn(__fadd_rn(__fadd_rn(-s1, -s2), s3), s4);
+      const float gz = __fadd_rn(__fadd_rn(__fadd_rn(-s1, s2), -s3), s4);
+      a.grad[3 * slot + 0] = gx / a.grad_den;
+      a.grad[3 * slot + 1] = gy / a.grad_den;
+      a.grad[3 * slot + 2] = gz / a.grad_den;
+      if (a.with_hessian) {
+        const float sum = __fadd_rn(__fadd_rn(__fadd_rn(s1, s2), s3), s4);
+        const float hxx = __fadd_rn(sum / 2.0f, -__fmul_rn(2.0f, s0)) / a.hess_den;
+        const float hv = hxx / 3.0f;
+        a.hess[3 * slot + 0] = hv;
+        a.hess[3 * slot + 1] = hv;
+        a.hess[3 * slot + 2] = hv;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- FIELD mode, fused
+// One launch for the whole FIELD: per wave a 32-sample tile at a time (grid-stride over the
+// tiles), the 5 points' encodings gathered level-outer exactly as encode5_kernel (taps reuse the
+// center's corners) but kept in registers (5 points x 8 k-steps x half8 = 160 VGPRs) instead of
+// an fp16 image in HBM, then layer 0 + softplus + sdf head per point from the LDS-resident
+// weights as field_mlp_kernel (same arithmetic: bit-identical sdf / grad / hess / h0).  One
+// 8-wave workgroup per CU (registers); waves in their gather phase (latency) and waves in their
+// MLP phase (VALU / MFMA) share each SIMD.  With a.enc set (stage a: the backward re-reads the
+// encodings) the image is written as well.
+
+// Layer 0 + softplus + sdf head of one point (as sdf_from_enc, with the row constants read four
+// at a time: fewer live registers beside the 160 of the encodings).
+MLI_FI float sdf_from_enc_lp(const uint8_t* lds, const half8 (&enc)[8], int lane, float px, float py, float pz,
+                             uint16_t* __restrict__ h0_tile) {
+  const int h = lane >> 5;
+  float part = 0.0f;
+#pragma unroll 1
+  for (int t = 0; t < 8; ++t) {
+    const f32x4* rc = reinterpret_cast<const f32x4*>(lds + ROWC_OFF + (t * 2 + h) * 64);
+    constexpr int A4 = ROWC_ARRAY / 16;  // f32x4 per array
+    f32x16 acc;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f32x4 b0 = rc[u], wx = rc[A4 + u], wy = rc[2 * A4 + u], wz = rc[3 * A4 + u];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[4 * u + j] = b0[j] + (wx[j] * px + wy[j] * py + wz[j] * pz);
+    }
+    const half8* frag = reinterpret_cast<const half8*>(lds + t * 8 * 1024) + lane;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc = mfma32(frag[q * 64], enc[q], acc);
+    f32x16 sp;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f32x4 ws = rc[4 * A4 + u];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sp[4 * u + j] = softplus100(acc[4 * u + j]);
+        part = fmaf(ws[j], sp[4 * u + j], part);
+      }
+    }
+    if (h0_tile) {  // read by the next kernel only: non-temporal
+      half8* dst = reinterpret_cast<half8*>(h0_tile) + (2 * t) * 64 + lane;
+      __builtin_nontemporal_store(acc_to_frag(sp, 0), dst);
+      __builtin_nontemporal_store(acc_to_frag(sp, 1), dst + 64);
+    }
+  }
+  part += __shfl_xor(part, 32);
+  return part + *reinterpret_cast<const float*>(lds + BSDF_OFF);
+}
+
+constexpr int FIELD_WAVES = 8;
+
+// Level pair QQ (levels 2QQ in lane half 0, 2QQ+1 in half 1) of the 5 points into enc[p][QQ]
+// (and the stage-a encoding image when ebase is set).
+template <int QQ>
+MLI_FI void field_gather_pair(const mli_sdf_args& a, int h, const float (&x)[TAPS][3], uint16_t* ebase,
+                              half8 (&enc)[TAPS][8]) {
+  const int lv0 = 2 * QQ, lv1 = 2 * QQ + 1;
+  auto sink = [&](int p, const half8& e) MLI_LAMBDA_FI {
+    enc[p][QQ] = e;
+    if (ebase) *reinterpret_cast<half8*>(ebase + ((size_t)p * 8 + QQ) * 512) = e;
+  };
+  if (lv0 >= a.active_levels) {  // coarse-to-fine: the whole level pair encodes to 0
+    half8 z;
+#pragma unroll
+    for (int f = 0; f < 8; ++f) z[f] = (f16)0.0f;
+#pragma unroll
+    for (int p = 0; p < TAPS; ++p) sink(p, z);
+    return;
+  }
+  const mli_grid_levels& L = a.levels;
+  const LevelP P0 = level_params(L, lv0), P1 = level_params(L, lv1);
+  const LevelP P{h ? P1.scale : P0.scale, h ? P1.res : P0.res, h ? P1.size : P0.size,
+                 h ? P1.offset : P0.offset, h ? P1.magic : P0.magic};
+  const bool d0 = level_dense(L, lv0), d1 = level_dense(L, lv1);
+  const bool keep = (h ? lv1 : lv0) < a.active_levels;
+  if (d0 && d1)
+    level5<0>(a.table, P, x, keep, sink);
+  else if (!d0 && !d1)
+    level5<1>(a.table, P, x, keep, sink);
+  else
+    level5<2>(a.table, P, x, keep, sink);
+}
+
+__global__ __launch_bounds__(FIELD_WAVES * 64) void field_kernel(mli_sdf_args a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  load_weights(lds, a.wsdf);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int n_total = a.R * a.n_per_ray;
+  const int n_tiles = (n_total + 31) >> 5;
+  for (int tile = blockIdx.x * FIELD_WAVES + wave; tile < n_tiles; tile += gridDim.x * FIELD_WAVES) {
+    const uint8_t* lds_t = lds + opaque_v(0);  // keep LDS fragments from being hoisted (registers)
+    const int m = tile * 32 + c;
+    const bool valid = m < n_total;
+    const int mm = valid ? m : n_total - 1;
+    const int r = mm / a.n_per_ray, k = mm - r * a.n_per_ray;
+    const int slot = k * a.R + r;
+    float q[TAPS][3];
+    field_points(a, slot, r, q);
+    half8 enc[TAPS][8];
+    {
+      float x[TAPS][3];
+#pragma unroll
+      for (int p = 0; p < TAPS; ++p)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) x[p][d] = (q[p][d] + 2.0f) * 0.25f;  // modules.py:82-83
+      uint16_t* ebase = a.enc ? a.enc + ((size_t)tile * TAPS * 8) * 512 + lane * 8 : nullptr;
+      // level pairs unrolled by template (the loop body is too large for the unroller, and a
+      // runtime k-step index would put the encodings in scratch)
+      auto pairs = [&](auto... qs) MLI_LAMBDA_FI { (field_gather_pair<decltype(qs)::value>(a, h, x, ebase, enc), ...); };
+      pairs(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{},
+            std::integral_constant<int, 3>{}, std::integral_constant<int, 4>{}, std::integral_constant<int, 5>{},
+            std::integral_constant<int, 6>{}, std::integral_constant<int, 7>{});
+    }
+    uint16_t* h0_tile = a.h0 + (size_t)tile * (16 * 64 * 8);
+    float s[TAPS];
+#pragma unroll
+    for (int pi = 0; pi < TAPS; ++pi)
+      s[pi] = sdf_from_enc_lp(lds_t, enc[pi], lane, q[pi][0], q[pi][1], q[pi][2], pi == 0 ? h0_tile : nullptr);
     float s0 = s[0];
     const float s1 = s[1], s2 = s[2], s3 = s[3], s4 = s[4];
     if (a.outside[r]) s0 = a.outside_val;

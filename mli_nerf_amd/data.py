@@ -60,6 +60,35 @@ def world_to_camera(c2w_gl, readjust=None):
     return invert_pose(c2w[:3])
 
 
+def transforms_cameras(meta, H, W, readjust=None, frames=None):
+    """[(intr [3,3], pose [3,4], pose_light [3,4])] of a ReNe-style transforms dict at image size
+    H x W, as Dataset.get_camera + preprocess_camera + get_light give them (neuralangelo
+    data.py:116-141, NeuralLumen/data.py:30-43): intrinsics from fl_x / sk_x / cx / sk_y / fl_y / cy
+    rescaled from the raw ``w`` x ``h`` (the size of the scene's images), GL->CV world-to-camera poses
+    of ``transform_matrix`` / ``transform_matrix_light``."""
+    intr0 = torch.tensor([[meta["fl_x"], meta["sk_x"], meta["cx"]], [meta["sk_y"], meta["fl_y"], meta["cy"]],
+                          [0, 0, 1]]).float()
+    intr0[0] *= W / meta["w"]
+    intr0[1] *= H / meta["h"]
+    out = []
+    for fr in (meta["frames"] if frames is None else [meta["frames"][i] for i in frames]):
+        out.append((intr0.clone(), world_to_camera(fr["transform_matrix"], readjust),
+                    world_to_camera(fr["transform_matrix_light"], readjust)))
+    return out
+
+
+# the real cameras of BASELINE.json configs[3] (rene_savannah_b): the reference's first 16
+# savannah training frames (tests/golden/make_rene_savannah.py)
+RENE_SAVANNAH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                             "rene_savannah_train16.json")
+
+
+def rene_savannah_cameras(H=270, W=360, frames=None):
+    with open(RENE_SAVANNAH) as f:
+        meta = json.load(f)
+    return transforms_cameras(meta, H, W, frames=frames)
+
+
 # --------------------------------------------------------------------------- images
 def to_tensor(img):
     """torchvision to_tensor on a PIL image: [C,H,W] float in [0,1] (8-bit) or as stored."""

@@ -117,13 +117,19 @@ class FusedAdamW:
         self.v = torch.zeros_like(flat.detach())
         self.step_count = 0
 
-    def step(self, grad, lr, p16=None):
+    def step(self, grad, lr, p16=None, ranges=None):
         """``p16``: fp16 tensor to receive a copy of the updated parameters (the hash table's
-        gather shadow), or None."""
+        gather shadow), or None.  ``ranges``: [(offset, n)] of the trainable elements when only
+        part of the buffer trains (the rest -- frozen by partial_grad / partial_training -- gets
+        no update, no weight decay and keeps its moments, as torch AdamW skips a parameter whose
+        grad is None); None: the whole buffer."""
         self.step_count += 1
-        L.call("mli_adamw", L.AdamwArgs(L.ptr(self.flat.detach()), L.ptr(grad), L.ptr(self.m), L.ptr(self.v),
-                                        self.flat.numel(), float(lr), self.betas[0], self.betas[1], self.eps,
-                                        self.wd, self.step_count, L.ptr(p16)))
+        p = self.flat.detach()
+        for off, n in ([(0, p.numel())] if ranges is None else ranges):
+            L.call("mli_adamw", L.AdamwArgs(L.ptr(p[off:]), L.ptr(grad[off:]), L.ptr(self.m[off:]),
+                                            L.ptr(self.v[off:]), n, float(lr), self.betas[0], self.betas[1],
+                                            self.eps, self.wd, self.step_count,
+                                            L.ptr(None if p16 is None else p16[off:])))
 
     def resize(self, numel):
         """Moments for a parameter whose size changed (a table-size rule switch on load)."""
@@ -311,6 +317,32 @@ class Trainer:
             if kw:
                 p.requires_grad_(any(k in name for k in kw))
 
+    def adam_ranges(self):
+        """[(offset, n)] of the flat buffer the optimizer steps: the Parameters of
+        model.get_param_groups(cfg.optim) whose requires_grad is on (NeuralLumen/trainer.py:44-54
+        partial_grad, NeuralLumen/model.py:422-438 partial_training), adjacent ones merged; None when
+        that is the whole buffer (one launch)."""
+        live = {n for n, p in self.optimized_parameters() if p.requires_grad}
+        items = self.model._trainable_items()
+        key = tuple(sorted(live))
+        if getattr(self, "_ranges_key", None) == key:
+            return self._ranges
+        ranges = []
+        for name, _, off, n in items:
+            if name in live:
+                if ranges and ranges[-1][0] + ranges[-1][1] == off:
+                    ranges[-1] = (ranges[-1][0], ranges[-1][1] + n)
+                else:
+                    ranges.append((off, n))
+        full = ranges == [(0, self.model.flat.numel())]
+        self._ranges_key, self._ranges = key, None if full else ranges
+        return self._ranges
+
+    def table_trains(self):
+        """Stage a: whether the hash table is among the optimized, requires_grad parameters."""
+        t = self.model.neural_sdf.tcnn_encoding.params
+        return any(p is t and p.requires_grad for _, p in self.optimized_parameters())
+
     def optimized_parameters(self):
         """[(name, Parameter)] of the reference optimizer, in its order:
         model.get_param_groups(cfg.optim) (get_trainer.py:106-118)."""
@@ -491,7 +523,7 @@ class Trainer:
             self._gate_ev, eng.gate_event = eng.gate_event, None
         reduce_gradients(self._grad, self.world_size)   # gradients + metrics, one collective
         m.set_flat_grad(grad)
-        self.optim.step(grad, self.lr())
+        self.optim.step(grad, self.lr(), ranges=self.adam_ranges())
         self.current_iteration += 1
         self._publish(lv)
         return m.outputs(st) if return_outputs else None
@@ -564,8 +596,9 @@ class Trainer:
         gtab = reduce_gradients(self._grad_table, self.world_size)
         m.set_flat_grad(grad)
         lr = self.lr()
-        self.optim.step(grad, lr)
-        self.optim_table.step(gtab, lr, p16=eng.table16)
+        self.optim.step(grad, lr, ranges=self.adam_ranges())
+        if self.table_trains():
+            self.optim_table.step(gtab, lr, p16=eng.table16)
         self.current_iteration += 1
         self._publish(lv)
         return m.outputs(st) if return_outputs else None
@@ -595,8 +628,8 @@ class Trainer:
         lv[5], lv[6] = total.detach(), psnr.detach()
         reduce_gradients(self._grad, self.world_size)
         m.set_flat_grad(grad)
-        self.optim.step(grad, self.lr())
-        if self.stage == "a":
+        self.optim.step(grad, self.lr(), ranges=self.adam_ranges())
+        if self.stage == "a" and self.table_trains():
             table = m.neural_sdf.tcnn_encoding.params
             gtab = reduce_gradients(table.grad, self.world_size)
             self.optim_table.step(gtab, self.lr(), p16=m.engine.table16)

@@ -94,16 +94,18 @@ def stub_losses(trainer, st, data, lv):
     return d_rgb, z, z[:, :1], z
 
 
-def stub_adamw_step(self, grad, lr, p16=None):
-    """torch.optim.AdamW's update on the flat buffer (FusedAdamW.step's semantics)."""
+def stub_adamw_step(self, grad, lr, p16=None, ranges=None):
+    """torch.optim.AdamW's update on the flat buffer (FusedAdamW.step's semantics, incl. ranges)."""
     self.step_count += 1
     b1, b2 = self.betas
-    p = self.flat.detach()
-    p.mul_(1 - lr * self.wd)
-    self.m.mul_(b1).add_(grad, alpha=1 - b1)
-    self.v.mul_(b2).addcmul_(grad, grad, value=1 - b2)
-    denom = (self.v / (1 - b2 ** self.step_count)).sqrt_().add_(self.eps)
-    p.addcdiv_(self.m, denom, value=-lr / (1 - b1 ** self.step_count))
+    for off, n in ([(0, self.flat.numel())] if ranges is None else ranges):
+        p, g = self.flat.detach()[off:off + n], grad[off:off + n]
+        m, v = self.m[off:off + n], self.v[off:off + n]
+        p.mul_(1 - lr * self.wd)
+        m.mul_(b1).add_(g, alpha=1 - b1)
+        v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        denom = (v / (1 - b2 ** self.step_count)).sqrt_().add_(self.eps)
+        p.addcdiv_(m, denom, value=-lr / (1 - b1 ** self.step_count))
 
 
 def install(monkeypatch=None):

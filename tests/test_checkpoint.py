@@ -122,3 +122,25 @@ def test_checkpointer_adapter_as_test_py_calls_it(tmp_path):
     assert torch.equal(m3.s_var, m.s_var)
     with pytest.raises(FileNotFoundError):
         tr3.checkpointer.load(str(tmp_path / "nope.pt"), False)
+
+
+def test_adam_ranges_follow_partial_grad():
+    """The fused AdamW steps exactly the optimized parameters whose requires_grad is on
+    (NeuralLumen/trainer.py:44-54): the whole flat buffer by default (one launch), the named head
+    alone with partial_grad = ['neural_rgb.mlp_r'], adjacent parameters merged into one range."""
+    from mli_nerf_amd.trainer import Trainer
+    cfg, m = _model("b")
+    tr = Trainer(cfg, is_inference=False, model=m)
+    assert tr.adam_ranges() is None
+    cfg2, m2 = _model("b")
+    cfg2.trainer["partial_grad"] = ["neural_rgb.mlp_r"]
+    tr2 = Trainer(cfg2, is_inference=False, model=m2)
+    items = {n: (off, k) for n, _, off, k in m2._trainable_items()}
+    mine = sorted(v for n, v in items.items() if n.startswith("neural_rgb.mlp_r."))
+    lo, hi = mine[0][0], mine[-1][0] + mine[-1][1]
+    assert tr2.adam_ranges() == [(lo, hi - lo)]
+    assert hi - lo == sum(k for _, k in mine)          # the head's parameters are contiguous
+    cfg3, m3 = _model("a")
+    cfg3.trainer["partial_grad"] = ["neural_rgb"]       # stage a with the SDF frozen: no table step
+    tr3 = Trainer(cfg3, is_inference=False, model=m3)
+    assert not tr3.table_trains() and tr3.adam_ranges() is not None

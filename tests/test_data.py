@@ -211,3 +211,32 @@ def test_device_feed_validates_shapes():
         f.sample(0, 1, 11)
     with pytest.raises(IndexError):
         f.sample(2, 1, 4)
+
+
+def test_rene_savannah_cameras_match_dataset(tmp_path):
+    """The savannah bench / full-size test cameras (data.rene_savannah_cameras, from the committed
+    frames of dataset_rene/savannah/train_transforms.json) equal what data.Dataset builds from the
+    same JSON with images of the scene's raw size, at rene_savannah_b's 270 x 360."""
+    import json as _json
+    from PIL import Image
+    from mli_nerf_amd import data as D
+    from mli_nerf_amd.configs import preset
+    meta = _json.load(open(D.RENE_SAVANNAH))
+    assert meta["w"] == 1440 and meta["h"] == 1080 and len(meta["frames"]) == 16
+    root = tmp_path / "savannah"
+    for fr in meta["frames"][:3]:
+        p = root / fr["file_path"]
+        p.parent.mkdir(parents=True, exist_ok=True)
+        Image.new("RGB", (meta["w"], meta["h"]), (255, 255, 255)).save(p)
+    ann = tmp_path / "train_transforms.json"
+    ann.write_text(_json.dumps(dict(meta, frames=meta["frames"][:3])))
+    cfg = preset("rene_savannah_b")
+    cfg.data["root"] = str(root)
+    cfg.data.train["annotation"] = str(ann)
+    ds = D.Dataset(cfg)
+    cams = D.rene_savannah_cameras(270, 360, frames=[0, 1, 2])
+    for i in range(3):
+        intr, pose = ds.preprocess_camera(*ds.get_camera(i), (meta["w"], meta["h"]))
+        assert torch.equal(intr, cams[i][0]) and torch.equal(pose, cams[i][1]) and torch.equal(ds.get_light(i), cams[i][2])
+    # the AABB the fixture's scene declares is the preset's (rene_savannah_b.yaml:53-60)
+    assert meta["bounding_box_aabb"] == list(cfg.data.bounding_box_aabb)

@@ -159,3 +159,27 @@ def test_overwritten_render_state_raises():
     with pytest.raises(RuntimeError, match="overwritten"):
         _losses(tr, out0, d0)[0].backward()
     _losses(tr, out1, d1)[0].backward()   # the latest render still backpropagates
+
+
+def test_partial_grad_steps_only_the_named_head():
+    """partial_grad = ['neural_rgb.mlp_r'] (NeuralLumen/trainer.py:44-54): the fused step updates
+    mlp_r and leaves the other two heads bit-unchanged (no update, no weight decay), their AdamW
+    moments zero -- torch AdamW skips a parameter whose grad is None."""
+    cfg, m = _model()
+    cfg.trainer["partial_grad"] = ["neural_rgb.mlp_r"]
+    tr = Trainer(cfg, is_inference=False, model=m)
+    before = {n: p.detach().clone() for n, p in m.named_parameters() if n.startswith("neural_rgb")}
+    for step in range(2):
+        d, u = _batch(step)
+        tr.train_step(d, u=u)
+    torch.cuda.synchronize()
+    items = {n: (off, k) for n, _, off, k in m._trainable_items()}
+    for n, p in m.named_parameters():
+        if not n.startswith("neural_rgb"):
+            continue
+        off, k = items[n]
+        if n.startswith("neural_rgb.mlp_r."):
+            assert not torch.equal(p.detach(), before[n]), n
+        else:
+            assert torch.equal(p.detach(), before[n]), n
+            assert not tr.optim.m[off:off + k].any() and not tr.optim.v[off:off + k].any(), n

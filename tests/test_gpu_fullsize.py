@@ -4,8 +4,8 @@ table.  The CPU oracle cannot run whole batches of this size in seconds, so each
 
 * a subset of the rays compared with the oracle conditioned on the GPU's own sample depths
   (the hierarchical sampler is chaotic; it is parity-tested round by round in
-  test_gpu_parity.py), at the end-to-end tolerances of test_gpu_parity.py: per output max abs
-  2e-2, mean abs 5e-4, PSNR of the difference >= 50 dB;
+  test_gpu_parity.py), at SURVEY §8(d)'s bar for a reduced-precision MFMA path: per output max
+  abs 2e-3 (measured ~1e-4), mean abs 5e-4, PSNR of the difference >= 50 dB;
 * size-independent properties of the whole batch: every output finite, compositing weights
   >= 0 with sum <= 1 per ray, per-ray results independent of the batch they are rendered in
   (bit-identical to a subset render), and -- for the gradient -- linearity: the render-loss
@@ -13,7 +13,8 @@ table.  The CPU oracle cannot run whole batches of this size in seconds, so each
   (cosine >= 0.9999), one of which is checked against the oracle's gradient (cosine >= 0.99,
   test_gpu_parity.py's bar);
 * the bench's PSNR check as a test: train-step PSNR on 512 rays x 128 samples, GPU vs oracle,
-  within 0.01 dB.
+  within 0.01 dB; and free-running (both sides sample on their own) at configs[2]'s full
+  8192 x 192 batch, within 0.01 dB.
 """
 import math
 
@@ -28,6 +29,7 @@ from oracle import render as o_render
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
+MAX_ABS = 2e-3   # composites of a reduced-precision MFMA path vs the fp32 oracle
 
 
 def _setup(config, R, Nf, log2T=22, frame=3):
@@ -39,7 +41,8 @@ def _setup(config, R, Nf, log2T=22, frame=3):
     data = synthetic.make_batch(R, H=H, W=W, frame=frame)
     box = cfg.data.get("bounding_type", "unit_sphere") == "box"
     pcfg = o_render.PathCfg(n_coarse=64, n_fine=Nf, log2T=log2T, white_bg=bool(cfg.model.background.white),
-                            bounding="box" if box else "sphere")
+                            bounding="box" if box else "sphere",
+                            aabb=tuple(cfg.data.get("bounding_box_aabb", (-1, -1, -1, 1, 1, 1))))
     sd16 = dict(sd)
     sd16["neural_sdf.tcnn_encoding.params"] = sd["neural_sdf.tcnn_encoding.params"].half().float()
     return cfg, m.to(DEV), sd16, data, pcfg, (H, W)
@@ -70,7 +73,7 @@ def _compare_subset(out, data, idx, sd16, pcfg, hw, u=None, training=True, sd_gr
         d = (out[key].detach()[:, idx].cpu() - o[key].detach()).abs()
         psnr_d = -10 * math.log10(max(float((d ** 2).mean()), 1e-20))
         print("%s max %.3g mean %.3g psnr(diff) %.1f dB" % (key, d.max(), d.mean(), psnr_d))
-        assert d.max() < 2e-2 and d.mean() < 5e-4 and psnr_d > 50, key
+        assert d.max() <= MAX_ABS and d.mean() < 5e-4 and psnr_d > 50, key
     return o
 
 
@@ -140,6 +143,48 @@ def test_config3_pikachu_full_batch():
     assert torch.isfinite(model.flat.grad).all() and model.flat.grad.abs().sum() > 0
     # the step ran at iteration 10000: progress 0.02, NeuS iter_cos anneal 0.2
     _compare_subset(out, data, torch.arange(0, R, 64), sd16, pcfg, hw, u=u, progress=model.progress)
+    # free-running train PSNR of the whole 8192 x 192 batch (each side samples on its own)
+    psnr_gpu = float(tr.metrics["psnr"])
+    with torch.no_grad():
+        torch.set_num_threads(min(16, torch.get_num_threads()))
+        o = o_render.forward(sd16, pcfg, data, u=u, training=True, progress=model.progress, width=hw[1],
+                             height=hw[0])
+    _, _, psnr_cpu = o_render.stage_b_losses(o, data, pcfg)
+    print("config 3 free-running train PSNR gpu %.5f cpu %.5f" % (psnr_gpu, float(psnr_cpu)))
+    assert abs(psnr_gpu - float(psnr_cpu)) <= 0.01
+
+
+@pytest.mark.timeout(900)
+def test_config4_savannah_real_poses():
+    """configs[3]: rene_savannah_b at its own workload -- 4096 rays x 128 samples per rank,
+    270 x 360, AABB bounds (rene_savannah_b.yaml:53-60) and the reference's REAL savannah camera +
+    light of frame 0 (rank 0; dataset_rene/savannah/train_transforms.json), full table, one fused
+    train step: batch properties, a ray subset against the oracle on the GPU's depths, and per-ray
+    batch independence of the render (a subset rendered alone is bit-identical)."""
+    from mli_nerf_amd.data import rene_savannah_cameras
+    from mli_nerf_amd.trainer import Trainer
+    R, N = 4096, 128
+    cfg, model, sd16, _, pcfg, hw = _setup("rene_savannah_b", R, 16)
+    intr, pose, light = rene_savannah_cameras(*hw, frames=[0])[0]
+    data = synthetic.make_batch(R, H=hw[0], W=hw[1], frame=0, poses=(pose, light, intr))
+    u = torch.rand(1, R, 64, generator=torch.Generator().manual_seed(11))
+    tr = Trainer(cfg, is_inference=False, model=model)
+    tr.current_iteration = 10000
+    out = tr.train_step({k: v.to(DEV) for k, v in data.items()}, u=u.to(DEV), return_outputs=True)
+    torch.cuda.synchronize()
+    _check_properties(out, R, N)
+    inside = (~out["outside"][0, :, 0]).float().mean().item()
+    print("savannah frame 0: %.1f %% of the rays hit the AABB" % (100 * inside))
+    assert inside > 0.05           # the real camera looks into the box (frame 0: every ray hits it)
+    assert all(math.isfinite(float(v)) for v in tr.losses.values())
+    assert torch.isfinite(model.flat.grad).all() and model.flat.grad.abs().sum() > 0
+    full = {k: out[k].detach().clone() for k in ("rgb", "o_r", "o_s", "o_re", "dists")}
+    _compare_subset(full, data, torch.arange(0, R, 32), sd16, pcfg, hw, u=u, progress=model.progress)
+    model.train()
+    idx = torch.arange(5, R, 7)
+    o_k = model(_subset({k: v.to(DEV) for k, v in data.items()}, idx.to(DEV)), u=u[:, idx].to(DEV))
+    for key in ("rgb", "o_r", "o_s", "o_re", "dists"):
+        assert torch.equal(o_k[key].detach(), full[key][:, idx.to(DEV)]), key
 
 
 @pytest.mark.timeout(900)
@@ -174,7 +219,7 @@ def test_config5_frame_800():
         d = (out[key].cpu() - o[key]).abs()
         psnr_d = -10 * math.log10(max(float((d ** 2).mean()), 1e-20))
         print("800^2 %s max %.3g mean %.3g psnr(diff) %.1f dB" % (key, d.max(), d.mean(), psnr_d))
-        assert d.max() < 2e-2 and d.mean() < 5e-4 and psnr_d > 50, key
+        assert d.max() <= MAX_ABS and d.mean() < 5e-4 and psnr_d > 50, key
 
 
 @pytest.mark.timeout(900)

@@ -222,7 +222,8 @@ def test_end_to_end_forward_backward(case):
         d = (out[key].detach().cpu() - o_out[key].detach()).abs()
         psnr_d = -10 * math.log10(max(float((d ** 2).mean()), 1e-20))
         print("%s %s max %.3g mean %.3g psnr(diff) %.1f dB" % (case, key, d.max(), d.mean(), psnr_d))
-        assert d.max() < 2e-2 and d.mean() < 5e-4 and psnr_d > 50, key
+        # max abs 2e-3 on composites for a reduced-precision MFMA path (measured ~1e-4)
+        assert d.max() <= 2e-3 and d.mean() < 5e-4 and psnr_d > 50, key
     assert abs(psnr.item() - o_psnr.item()) < 0.1, (psnr.item(), o_psnr.item())
     for k in ("render", "intrinsic", "regularize_re"):
         a, b = losses[k].item(), o_losses[k].item()
