@@ -60,14 +60,47 @@ MLI_FI half8 acc_to_frag(const f32x16& v, int s) {
   return __builtin_bit_cast(half8, w);
 }
 
+// torch.nn.functional.softplus(x, beta=100, threshold=20) as max(x, 0) + log(1 + e^{-|t|}) / 100,
+// t = 100 x, on the raw v_exp_f32 / v_log_f32 (base 2: log2(1 + 2^{-|t| log2 e}) ln2 / 100; the
+// log argument is in [1, 2], never denormal).  The same function as the threshold form: where
+// the reference returns x (t > 20) this adds <= 2e-9 x 0.0069 (below an ulp of x), and the
+// -|t| of the exp is a free source modifier, so no compare / select and no overflow guard.
+// The pair form issues the multiplies / adds as packed fp32 (v_pk_mul_f32 / v_pk_add_f32 /
+// v_pk_fma_f32, two elements per lane per issue) and computes bit-identical values; the
+// layer-0 / layer-1 epilogues are VALU bound on this function.
+// max(x, 0) as one v_max_i32 on the bit pattern (every negative float, -0 included, is a
+// negative int32): fmaxf / fmed3 are lowered with a canonicalising v_max_f32 x, x first, a
+// second instruction per element on the softplus epilogues.  (Not inline asm: the hazard
+// recognizer does not see an asm operand read right after the MFMA that wrote it.)
+MLI_FI float relu_f(float x) {
+  const int b = __builtin_bit_cast(int, x);
+  return __builtin_bit_cast(float, b > 0 ? b : 0);
+}
+
 MLI_FI float softplus100(float x) {
-  // torch.nn.functional.softplus(x, beta=100, threshold=20) on the raw v_exp_f32 / v_log_f32
-  // (base 2; the log argument 1 + e^t >= 1 is never denormal, so the denormal-scaling
-  // expansion of logf is dead weight): log(1 + e^t) / 100 = log2(1 + 2^(t log2 e)) * ln2/100.
-  const float t = x * 100.0f;
-  const float e = __builtin_amdgcn_exp2f(t * 1.4426950408889634f);
-  const float sp = __builtin_amdgcn_logf(1.0f + e) * 0.0069314718055994531f;
-  return t > 20.0f ? x : sp;
+  const float u = x * 144.26950408889634f;  // 100 log2 e
+  const float l = __builtin_amdgcn_logf(__builtin_amdgcn_exp2f(-fabsf(u)) + 1.0f);
+  return fmaf(l, 0.0069314718055994531f, relu_f(x));
+}
+
+MLI_FI f32x2 softplus100x2(f32x2 x) {
+  const f32x2 u = x * (f32x2){144.26950408889634f, 144.26950408889634f};
+  f32x2 e;
+  e.x = __builtin_amdgcn_exp2f(-fabsf(u.x));
+  e.y = __builtin_amdgcn_exp2f(-fabsf(u.y));
+  const f32x2 a = e + (f32x2){1.0f, 1.0f};
+  f32x2 l;
+  l.x = __builtin_amdgcn_logf(a.x);
+  l.y = __builtin_amdgcn_logf(a.y);
+  return __builtin_elementwise_fma(l, (f32x2){0.0069314718055994531f, 0.0069314718055994531f},
+                                   (f32x2){relu_f(x.x), relu_f(x.y)});
+}
+
+// b0 + W[:, 0:3] . p on an element pair: three v_pk_fma_f32.
+MLI_FI f32x2 pterm_x2(f32x2 b0, f32x2 wx, f32x2 wy, f32x2 wz, float px, float py, float pz) {
+  f32x2 v = __builtin_elementwise_fma(wx, (f32x2){px, px}, b0);
+  v = __builtin_elementwise_fma(wy, (f32x2){py, py}, v);
+  return __builtin_elementwise_fma(wz, (f32x2){pz, pz}, v);
 }
 
 MLI_FI float sigmoidf_acc(float x) { return 1.0f / (1.0f + expf(-x)); }

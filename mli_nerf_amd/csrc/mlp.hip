@@ -436,7 +436,11 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
                                     [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
     f32x16 v;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = softplus100(acc[i]);
+    for (int i = 0; i < 16; i += 2) {
+      const f32x2 sp = softplus100x2((f32x2){acc[i], acc[i + 1]});
+      v[i] = sp.x;
+      v[i + 1] = sp.y;
+    }
     A[2 * t] = acc_to_frag(v, 0);
     A[2 * t + 1] = acc_to_frag(v, 1);
     half8* dst = reinterpret_cast<half8*>(ftile) + (2 * t) * 64 + lane;

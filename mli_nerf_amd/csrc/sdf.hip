@@ -90,31 +90,43 @@ MLI_FI void hash_encode(const uint16_t* __restrict__ table, const mli_grid_level
 
 // Layer 0 + softplus + sdf head from the encoding fragments.  Returns the full sdf (after
 // the cross-half reduction).  If h0_tile != nullptr the fp16 softplus activations are stored
-// as the frag image of this tile.
+// as the frag image of this tile.  The row constants are read four at a time (fewer live
+// registers); the pre-activation, softplus and sdf dot run on element pairs (packed fp32:
+// common.h softplus100x2 / pterm_x2).
 MLI_FI float sdf_from_enc(const uint8_t* lds, const half8 (&enc)[8], int lane, float px, float py, float pz,
                           uint16_t* __restrict__ h0_tile) {
   const int h = lane >> 5;
-  float part = 0.0f;
+  f32x2 part2 = {0.0f, 0.0f};
 #pragma unroll 1
   for (int t = 0; t < 8; ++t) {
-    float b0[16], wx[16], wy[16], wz[16];
-    load_rowc(lds, 0, t, h, b0);
-    load_rowc(lds, 1, t, h, wx);
-    load_rowc(lds, 2, t, h, wy);
-    load_rowc(lds, 3, t, h, wz);
+    const f32x4* rc = reinterpret_cast<const f32x4*>(lds + ROWC_OFF + (t * 2 + h) * 64);
+    constexpr int A4 = ROWC_ARRAY / 16;  // f32x4 per array
     f32x16 acc;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = b0[i] + (wx[i] * px + wy[i] * py + wz[i] * pz);
+    for (int u = 0; u < 4; ++u) {
+      const f32x4 b0 = rc[u], wx = rc[A4 + u], wy = rc[2 * A4 + u], wz = rc[3 * A4 + u];
+#pragma unroll
+      for (int j = 0; j < 4; j += 2) {
+        const f32x2 v = pterm_x2((f32x2){b0[j], b0[j + 1]}, (f32x2){wx[j], wx[j + 1]}, (f32x2){wy[j], wy[j + 1]},
+                                 (f32x2){wz[j], wz[j + 1]}, px, py, pz);
+        acc[4 * u + j] = v.x;
+        acc[4 * u + j + 1] = v.y;
+      }
+    }
     const half8* frag = reinterpret_cast<const half8*>(lds + t * 8 * 1024) + lane;
 #pragma unroll
     for (int q = 0; q < 8; ++q) acc = mfma32(frag[q * 64], enc[q], acc);
-    float ws[16];
-    load_rowc(lds, 4, t, h, ws);
     f32x16 sp;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      sp[i] = softplus100(acc[i]);
-      part = fmaf(ws[i], sp[i], part);
+    for (int u = 0; u < 4; ++u) {
+      const f32x4 ws = rc[4 * A4 + u];
+#pragma unroll
+      for (int j = 0; j < 4; j += 2) {
+        const f32x2 v = softplus100x2((f32x2){acc[4 * u + j], acc[4 * u + j + 1]});
+        sp[4 * u + j] = v.x;
+        sp[4 * u + j + 1] = v.y;
+        part2 = __builtin_elementwise_fma((f32x2){ws[j], ws[j + 1]}, v, part2);
+      }
     }
     if (h0_tile) {  // read by the next kernel only: non-temporal
       half8* dst = reinterpret_cast<half8*>(h0_tile) + (2 * t) * 64 + lane;
@@ -122,6 +134,7 @@ MLI_FI float sdf_from_enc(const uint8_t* lds, const half8 (&enc)[8], int lane, f
       __builtin_nontemporal_store(acc_to_frag(sp, 1), dst + 64);
     }
   }
+  float part = part2.x + part2.y;
   part += __shfl_xor(part, 32);
   return part + *reinterpret_cast<const float*>(lds + BSDF_OFF);
 }
@@ -141,82 +154,136 @@ MLI_FI float sdf_point(const uint8_t* lds, const uint16_t* __restrict__ table, c
 // hash_level (bit-identical encodings), written as B-fragment images for phase B.
 constexpr int TAPS = 5;
 
-// sink(p, e): the fp16 encoding e (8 features of this lane's level) of point p
-template <int KIND, class Sink>
-MLI_FI void level5(const uint16_t* __restrict__ table, const LevelP& P, const float (&x)[TAPS][3], bool keep,
-                   Sink&& sink) {
-  const uint32_t r2 = P.res * P.res;
-  const bool dense_lane = (uint64_t)P.res * P.res * P.res <= (uint64_t)P.size;
-  auto index_of = [&](uint32_t cx, uint32_t cy, uint32_t cz, bool skip_mod) MLI_LAMBDA_FI {
-    const uint32_t lin = cx + cy * P.res + cz * r2;
-    const uint32_t hsh = (cx ^ (cy * 2654435761u) ^ (cz * 805459861u)) & (P.size - 1u);
-    if (KIND == 1) return hsh;
-    const uint32_t dn = skip_mod ? lin : fastmod_u32(lin, P.magic, P.size);
-    return KIND == 0 ? dn : (dense_lane ? dn : hsh);
-  };
-  auto cell = [&](const float (&xp)[3], uint32_t (&g)[3], float (&pos)[3]) MLI_LAMBDA_FI {
+// The 5 points' encodings at one level pair (lane half h = level 2qq+h), taps' own gathers
+// compacted across the wave.  The center's 8 corners are gathered once and every tap in the
+// center's cell interpolates them with its own weights.  A per-tap gather on the lanes whose tap
+// left the cell (the straightforward form) costs up to 5 dependent gather rounds of mostly idle
+// lanes per level pair at the fine levels (SQ counters: 213 gather instructions per 32-sample
+// tile, waves parked 82 % of their cycles).  Instead every (tap, lane) whose cell differs from
+// the center's becomes a job: its tap position goes to a wave-private LDS list (ballot + mbcnt
+// slots, taps in order, lanes ascending) and the wave runs the jobs 64 at a time, one per lane,
+// with the job's own level (the source lane's half) -- 8 fully used gathers per job round,
+// issued beside the center's.  FIELD -4 % (0.832 -> 0.798 ms): the gather request count is
+// unchanged, and that, not the round trips, is most of the bound.  The interpolation of every
+// (point, level) is one function (interp8) on the same inputs whichever lane runs it.
+// sink(p, src_lane, e) stores point p of lane src_lane.
+struct TapJob {
+  float x0, x1, x2;
+  uint32_t tag;  // (p << 8) | source lane
+};
+
+template <int KIND>
+MLI_FI uint32_t corner_index(const LevelP& P, uint32_t cx, uint32_t cy, uint32_t cz, bool skip_mod) {
+  const uint32_t lin = cx + cy * P.res + cz * (P.res * P.res);
+  const uint32_t hsh = (cx ^ (cy * 2654435761u) ^ (cz * 805459861u)) & (P.size - 1u);
+  if (KIND == 1) return hsh;
+  const uint32_t dn = skip_mod ? lin : fastmod_u32(lin, P.magic, P.size);
+  if (KIND == 0) return dn;
+  return (uint64_t)P.res * P.res * P.res <= (uint64_t)P.size ? dn : hsh;
+}
+
+MLI_FI void grid_cell(const LevelP& P, const float (&xp)[3], uint32_t (&g)[3], float (&pos)[3]) {
 #pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      const float p = fmaf(P.scale, xp[d], 0.5f);  // tcnn pos_fract
-      const float fl = floorf(p);
-      g[d] = (uint32_t)(int)fl;
-      pos[d] = p - fl;
-    }
-  };
-  auto interp_store = [&](const u32x4 (&cv)[8], const float (&pos)[3], int pt) MLI_LAMBDA_FI {
-    float acc[8];
+  for (int d = 0; d < 3; ++d) {
+    const float q = fmaf(P.scale, xp[d], 0.5f);  // tcnn pos_fract
+    const float fl = floorf(q);
+    g[d] = (uint32_t)(int)fl;
+    pos[d] = q - fl;
+  }
+}
+
+MLI_FI half8 interp8(const u32x4 (&cv)[8], const float (&pos)[3], bool keep) {
+  float acc[8];
 #pragma unroll
-    for (int f = 0; f < 8; ++f) acc[f] = 0.0f;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      float w = 1.0f;
-      w *= (c & 1) ? pos[0] : 1.0f - pos[0];
-      w *= ((c >> 1) & 1) ? pos[1] : 1.0f - pos[1];
-      w *= ((c >> 2) & 1) ? pos[2] : 1.0f - pos[2];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f16 lo = __builtin_bit_cast(f16, (uint16_t)(cv[c][q] & 0xFFFFu));
-        const f16 hi = __builtin_bit_cast(f16, (uint16_t)(cv[c][q] >> 16));
-        acc[2 * q] = fmaf(w, (float)lo, acc[2 * q]);
-        acc[2 * q + 1] = fmaf(w, (float)hi, acc[2 * q + 1]);
-      }
-    }
-    half8 e;
-#pragma unroll
-    for (int f = 0; f < 8; ++f) e[f] = (f16)(keep ? acc[f] : 0.0f);  // c2f mask
-    sink(pt, e);
-  };
-  // center
-  uint32_t g0[3];
-  float pos0[3];
-  cell(x[0], g0, pos0);
-  const bool in_grid = g0[0] + 1 < P.res && g0[1] + 1 < P.res && g0[2] + 1 < P.res;
-  const bool skip_mod = KIND == 0 && __all(in_grid);
-  u32x4 cc[8];
+  for (int f = 0; f < 8; ++f) acc[f] = 0.0f;
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
-    const uint32_t idx = index_of(g0[0] + (c & 1), g0[1] + ((c >> 1) & 1), g0[2] + ((c >> 2) & 1), skip_mod);
-    cc[c] = *reinterpret_cast<const u32x4*>(table + (size_t)(P.offset + idx) * 8);
+    float w = 1.0f;
+    w *= (c & 1) ? pos[0] : 1.0f - pos[0];
+    w *= ((c >> 1) & 1) ? pos[1] : 1.0f - pos[1];
+    w *= ((c >> 2) & 1) ? pos[2] : 1.0f - pos[2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f16 lo = __builtin_bit_cast(f16, (uint16_t)(cv[c][q] & 0xFFFFu));
+      const f16 hi = __builtin_bit_cast(f16, (uint16_t)(cv[c][q] >> 16));
+      acc[2 * q] = fmaf(w, (float)lo, acc[2 * q]);
+      acc[2 * q + 1] = fmaf(w, (float)hi, acc[2 * q + 1]);
+    }
   }
-  interp_store(cc, pos0, 0);
-  // taps
+  half8 e;
+#pragma unroll
+  for (int f = 0; f < 8; ++f) e[f] = (f16)(keep ? acc[f] : 0.0f);  // c2f mask
+  return e;
+}
+
+template <int KIND>
+MLI_FI void gather8(const uint16_t* __restrict__ table, const LevelP& P, const uint32_t (&g)[3], bool skip_mod,
+                    u32x4 (&cv)[8]) {
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const uint32_t idx = corner_index<KIND>(P, g[0] + (c & 1), g[1] + ((c >> 1) & 1), g[2] + ((c >> 2) & 1), skip_mod);
+    cv[c] = *reinterpret_cast<const u32x4*>(table + (size_t)(P.offset + idx) * 8);
+  }
+}
+
+// P: this lane's level (half h); P0 / P1: the pair's two levels (a job takes its source's);
+// keep0 / keep1: the coarse-to-fine masks of the two levels; jobs: this wave's LDS list.
+template <int KIND, class Sink>
+MLI_FI void level5(const uint16_t* __restrict__ table, const LevelP& P0, const LevelP& P1, int lane,
+                    const float (&x)[TAPS][3], bool keep0, bool keep1, TapJob* jobs, Sink&& sink) {
+  const int h = lane >> 5;
+  const LevelP P{h ? P1.scale : P0.scale, h ? P1.res : P0.res, h ? P1.size : P0.size, h ? P1.offset : P0.offset,
+                 h ? P1.magic : P0.magic};
+  const bool keep = h ? keep1 : keep0;
+  uint32_t g0[3];
+  float pos0[3];
+  grid_cell(P, x[0], g0, pos0);
+  // the job list: taps whose cell is not the center's
+  int n_jobs = 0;
 #pragma unroll
   for (int p = 1; p < TAPS; ++p) {
     uint32_t g[3];
     float pos[3];
-    cell(x[p], g, pos);
-    const bool same = g[0] == g0[0] && g[1] == g0[1] && g[2] == g0[2];
-    u32x4 tc[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) tc[c] = cc[c];
-    if (!same) {  // divergent: only the lanes whose tap left the center's cell gather
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const uint32_t idx = index_of(g[0] + (c & 1), g[1] + ((c >> 1) & 1), g[2] + ((c >> 2) & 1), false);
-        tc[c] = *reinterpret_cast<const u32x4*>(table + (size_t)(P.offset + idx) * 8);
-      }
+    grid_cell(P, x[p], g, pos);
+    const bool div = g[0] != g0[0] || g[1] != g0[1] || g[2] != g0[2];
+    const uint64_t mask = __ballot(div);
+    if (div) {
+      const int slot = n_jobs + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+      jobs[slot] = TapJob{x[p][0], x[p][1], x[p][2], (uint32_t)((p << 8) | lane)};
     }
-    interp_store(tc, pos, p);
+    n_jobs += __popcll(mask);
+  }
+  const bool in_grid = g0[0] + 1 < P.res && g0[1] + 1 < P.res && g0[2] + 1 < P.res;
+  const bool skip_mod = KIND == 0 && __all(in_grid);
+  u32x4 cc[8];
+  gather8<KIND>(table, P, g0, skip_mod, cc);
+  // job rounds: lane j runs job j0 + j with its source lane's level
+  for (int j0 = 0; j0 < n_jobs; j0 += 64) {
+    const int j = j0 + lane;
+    if (j < n_jobs) {
+      const TapJob jb = jobs[j];
+      const int src = (int)(jb.tag & 255u), p = (int)(jb.tag >> 8);
+      const int hs = src >> 5;
+      const LevelP Q{hs ? P1.scale : P0.scale, hs ? P1.res : P0.res, hs ? P1.size : P0.size,
+                     hs ? P1.offset : P0.offset, hs ? P1.magic : P0.magic};
+      const float xj[3] = {jb.x0, jb.x1, jb.x2};
+      uint32_t g[3];
+      float pos[3];
+      grid_cell(Q, xj, g, pos);
+      u32x4 tc[8];
+      gather8<KIND>(table, Q, g, false, tc);
+      sink(p, src, interp8(tc, pos, hs ? keep1 : keep0));
+    }
+  }
+  // the center, and every tap in the center's cell, from the center's corners
+  sink(0, lane, interp8(cc, pos0, keep));
+#pragma unroll
+  for (int p = 1; p < TAPS; ++p) {
+    uint32_t g[3];
+    float pos[3];
+    grid_cell(P, x[p], g, pos);
+    if (g[0] == g0[0] && g[1] == g0[1] && g[2] == g0[2]) sink(p, lane, interp8(cc, pos, keep));
   }
 }
 
@@ -241,8 +308,9 @@ MLI_FI void field_points(const mli_sdf_args& a, int slot, int r, float (&q)[TAPS
 }
 
 __global__ __launch_bounds__(256) void encode5_kernel(mli_sdf_args a, int tile0, int tile1) {
+  __shared__ TapJob job_lists[4][4 * 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = lane & 31, h = lane >> 5;
+  const int c = lane & 31;
   const int n_total = a.R * a.n_per_ray;
   const int tile = tile0 + blockIdx.x * 4 + wave;
   if (tile >= tile1) return;
@@ -255,37 +323,36 @@ __global__ __launch_bounds__(256) void encode5_kernel(mli_sdf_args a, int tile0,
   for (int p = 0; p < TAPS; ++p)
 #pragma unroll
     for (int d = 0; d < 3; ++d) x[p][d] = (q[p][d] + 2.0f) * 0.25f;  // modules.py:82-83
-  uint16_t* base = a.enc + ((size_t)tile * TAPS * 8) * 512 + lane * 8;
+  uint16_t* base = a.enc + ((size_t)tile * TAPS * 8) * 512;
   const mli_grid_levels& L = a.levels;
+  TapJob* jobs = job_lists[wave];
 #pragma unroll 1
   for (int qq = 0; qq < 8; ++qq) {
     const int lv0 = 2 * qq, lv1 = 2 * qq + 1;
-    const LevelP P0 = level_params(L, lv0), P1 = level_params(L, lv1);
-    const LevelP P{h ? P1.scale : P0.scale, h ? P1.res : P0.res, h ? P1.size : P0.size,
-                   h ? P1.offset : P0.offset, h ? P1.magic : P0.magic};
-    const bool d0 = level_dense(L, lv0), d1 = level_dense(L, lv1);
     uint16_t* dst = base + (size_t)qq * 512;
     if (lv0 >= a.active_levels) {  // coarse-to-fine: the whole level pair encodes to 0
 #pragma unroll
-      for (int p = 0; p < TAPS; ++p) *reinterpret_cast<u32x4*>(dst + (size_t)p * 8 * 512) = u32x4{0, 0, 0, 0};
+      for (int p = 0; p < TAPS; ++p)
+        *reinterpret_cast<u32x4*>(dst + (size_t)p * 8 * 512 + lane * 8) = u32x4{0, 0, 0, 0};
       continue;
     }
-    const bool keep = (h ? lv1 : lv0) < a.active_levels;
-    auto sink = [&](int p, const half8& e) MLI_LAMBDA_FI {
-      *reinterpret_cast<half8*>(dst + (size_t)p * 8 * 512) = e;
+    const LevelP P0 = level_params(L, lv0), P1 = level_params(L, lv1);
+    const bool keep0 = lv0 < a.active_levels, keep1 = lv1 < a.active_levels;
+    const bool d0 = level_dense(L, lv0), d1 = level_dense(L, lv1);
+    auto sink = [&](int p, int src, const half8& e) MLI_LAMBDA_FI {
+      *reinterpret_cast<half8*>(dst + (size_t)p * 8 * 512 + src * 8) = e;
     };
     if (d0 && d1)
-      level5<0>(a.table, P, x, keep, sink);
+      level5<0>(a.table, P0, P1, lane, x, keep0, keep1, jobs, sink);
     else if (!d0 && !d1)
-      level5<1>(a.table, P, x, keep, sink);
+      level5<1>(a.table, P0, P1, lane, x, keep0, keep1, jobs, sink);
     else
-      level5<2>(a.table, P, x, keep, sink);
+      level5<2>(a.table, P0, P1, lane, x, keep0, keep1, jobs, sink);
   }
 }
 
 // ---------------------------------------------------------------- FIELD mode, phase B
-constexpr int MLP_WAVES = 8;  // 8 waves share the 70 KiB LDS weight block: 2 blocks = 16 waves per CU
-
+template <int MLP_WAVES>
 __global__ __launch_bounds__(MLP_WAVES * 64) void field_mlp_kernel(mli_sdf_args a, int tile0, int tile1) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   load_weights(lds, a.wsdf);
@@ -322,150 +389,6 @@ __global__ __launch_bounds__(MLP_WAVES * 64) void field_mlp_kernel(mli_sdf_args 
 #pragma unroll
       for (int j = 0; j < TAPS; ++j) s[j] = pi == j ? v : s[j];
     }
-    float s0 = s[0];
-    const float s1 = s[1], s2 = s[2], s3 = s[3], s4 = s[4];
-    if (a.outside[r]) s0 = a.outside_val;
-    if (valid && h == 0) {
-      a.sdf[slot] = s0;
-      // (k1*s1 + k2*s2 + k3*s3 + k4*s4) / (4 eps), summed left to right per component.
-      const float gx = __fadd_rn(__fadd_rn(__fadd_rn(s1, -s2), -s3), s4);
-      const float gy = __fadd_rn(__fadd_rn(__fadd_rn(-s1, -s2), s3), s4);
-      const float gz = __fadd_rn(__fadd_rn(__fadd_rn(-s1, s2), -s3), s4);
-      a.grad[3 * slot + 0] = gx / a.grad_den;
-      a.grad[3 * slot + 1] = gy / a.grad_den;
-      a.grad[3 * slot + 2] = gz / a.grad_den;
-      if (a.with_hessian) {
-        const float sum = __fadd_rn(__fadd_rn(__fadd_rn(s1, s2), s3), s4);
-        const float hxx = __fadd_rn(sum / 2.0f, -__fmul_rn(2.0f, s0)) / a.hess_den;
-        const float hv = hxx / 3.0f;
-        a.hess[3 * slot + 0] = hv;
-        a.hess[3 * slot + 1] = hv;
-        a.hess[3 * slot + 2] = hv;
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------- FIELD mode, fused
-// One launch for the whole FIELD: per wave a 32-sample tile at a time (grid-stride over the
-// tiles), the 5 points' encodings gathered level-outer exactly as encode5_kernel (taps reuse the
-// center's corners) but kept in registers (5 points x 8 k-steps x half8 = 160 VGPRs) instead of
-// an fp16 image in HBM, then layer 0 + softplus + sdf head per point from the LDS-resident
-// weights as field_mlp_kernel (same arithmetic: bit-identical sdf / grad / hess / h0).  One
-// 8-wave workgroup per CU (registers); waves in their gather phase (latency) and waves in their
-// MLP phase (VALU / MFMA) share each SIMD.  With a.enc set (stage a: the backward re-reads the
-// encodings) the image is written as well.
-
-// Layer 0 + softplus + sdf head of one point (as sdf_from_enc, with the row constants read four
-// at a time: fewer live registers beside the 160 of the encodings).
-MLI_FI float sdf_from_enc_lp(const uint8_t* lds, const half8 (&enc)[8], int lane, float px, float py, float pz,
-                             uint16_t* __restrict__ h0_tile) {
-  const int h = lane >> 5;
-  float part = 0.0f;
-#pragma unroll 1
-  for (int t = 0; t < 8; ++t) {
-    const f32x4* rc = reinterpret_cast<const f32x4*>(lds + ROWC_OFF + (t * 2 + h) * 64);
-    constexpr int A4 = ROWC_ARRAY / 16;  // f32x4 per array
-    f32x16 acc;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const f32x4 b0 = rc[u], wx = rc[A4 + u], wy = rc[2 * A4 + u], wz = rc[3 * A4 + u];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[4 * u + j] = b0[j] + (wx[j] * px + wy[j] * py + wz[j] * pz);
-    }
-    const half8* frag = reinterpret_cast<const half8*>(lds + t * 8 * 1024) + lane;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) acc = mfma32(frag[q * 64], enc[q], acc);
-    f32x16 sp;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const f32x4 ws = rc[4 * A4 + u];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        sp[4 * u + j] = softplus100(acc[4 * u + j]);
-        part = fmaf(ws[j], sp[4 * u + j], part);
-      }
-    }
-    if (h0_tile) {  // read by the next kernel only: non-temporal
-      half8* dst = reinterpret_cast<half8*>(h0_tile) + (2 * t) * 64 + lane;
-      __builtin_nontemporal_store(acc_to_frag(sp, 0), dst);
-      __builtin_nontemporal_store(acc_to_frag(sp, 1), dst + 64);
-    }
-  }
-  part += __shfl_xor(part, 32);
-  return part + *reinterpret_cast<const float*>(lds + BSDF_OFF);
-}
-
-constexpr int FIELD_WAVES = 8;
-
-// Level pair QQ (levels 2QQ in lane half 0, 2QQ+1 in half 1) of the 5 points into enc[p][QQ]
-// (and the stage-a encoding image when ebase is set).
-template <int QQ>
-MLI_FI void field_gather_pair(const mli_sdf_args& a, int h, const float (&x)[TAPS][3], uint16_t* ebase,
-                              half8 (&enc)[TAPS][8]) {
-  const int lv0 = 2 * QQ, lv1 = 2 * QQ + 1;
-  auto sink = [&](int p, const half8& e) MLI_LAMBDA_FI {
-    enc[p][QQ] = e;
-    if (ebase) *reinterpret_cast<half8*>(ebase + ((size_t)p * 8 + QQ) * 512) = e;
-  };
-  if (lv0 >= a.active_levels) {  // coarse-to-fine: the whole level pair encodes to 0
-    half8 z;
-#pragma unroll
-    for (int f = 0; f < 8; ++f) z[f] = (f16)0.0f;
-#pragma unroll
-    for (int p = 0; p < TAPS; ++p) sink(p, z);
-    return;
-  }
-  const mli_grid_levels& L = a.levels;
-  const LevelP P0 = level_params(L, lv0), P1 = level_params(L, lv1);
-  const LevelP P{h ? P1.scale : P0.scale, h ? P1.res : P0.res, h ? P1.size : P0.size,
-                 h ? P1.offset : P0.offset, h ? P1.magic : P0.magic};
-  const bool d0 = level_dense(L, lv0), d1 = level_dense(L, lv1);
-  const bool keep = (h ? lv1 : lv0) < a.active_levels;
-  if (d0 && d1)
-    level5<0>(a.table, P, x, keep, sink);
-  else if (!d0 && !d1)
-    level5<1>(a.table, P, x, keep, sink);
-  else
-    level5<2>(a.table, P, x, keep, sink);
-}
-
-__global__ __launch_bounds__(FIELD_WAVES * 64) void field_kernel(mli_sdf_args a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  load_weights(lds, a.wsdf);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = lane & 31, h = lane >> 5;
-  const int n_total = a.R * a.n_per_ray;
-  const int n_tiles = (n_total + 31) >> 5;
-  for (int tile = blockIdx.x * FIELD_WAVES + wave; tile < n_tiles; tile += gridDim.x * FIELD_WAVES) {
-    const uint8_t* lds_t = lds + opaque_v(0);  // keep LDS fragments from being hoisted (registers)
-    const int m = tile * 32 + c;
-    const bool valid = m < n_total;
-    const int mm = valid ? m : n_total - 1;
-    const int r = mm / a.n_per_ray, k = mm - r * a.n_per_ray;
-    const int slot = k * a.R + r;
-    float q[TAPS][3];
-    field_points(a, slot, r, q);
-    half8 enc[TAPS][8];
-    {
-      float x[TAPS][3];
-#pragma unroll
-      for (int p = 0; p < TAPS; ++p)
-#pragma unroll
-        for (int d = 0; d < 3; ++d) x[p][d] = (q[p][d] + 2.0f) * 0.25f;  // modules.py:82-83
-      uint16_t* ebase = a.enc ? a.enc + ((size_t)tile * TAPS * 8) * 512 + lane * 8 : nullptr;
-      // level pairs unrolled by template (the loop body is too large for the unroller, and a
-      // runtime k-step index would put the encodings in scratch)
-      auto pairs = [&](auto... qs) MLI_LAMBDA_FI { (field_gather_pair<decltype(qs)::value>(a, h, x, ebase, enc), ...); };
-      pairs(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{},
-            std::integral_constant<int, 3>{}, std::integral_constant<int, 4>{}, std::integral_constant<int, 5>{},
-            std::integral_constant<int, 6>{}, std::integral_constant<int, 7>{});
-    }
-    uint16_t* h0_tile = a.h0 + (size_t)tile * (16 * 64 * 8);
-    float s[TAPS];
-#pragma unroll
-    for (int pi = 0; pi < TAPS; ++pi)
-      s[pi] = sdf_from_enc_lp(lds_t, enc[pi], lane, q[pi][0], q[pi][1], q[pi][2], pi == 0 ? h0_tile : nullptr);
     float s0 = s[0];
     const float s1 = s[1], s2 = s[2], s3 = s[3], s4 = s[4];
     if (a.outside[r]) s0 = a.outside_val;
@@ -640,9 +563,10 @@ MLI_FI void field_points5(const float* center, const float* ray_unit, float d, i
   }
 }
 
+constexpr int BWD_WAVES = 8;  // stage-a sdf_bwd_kernel: waves per workgroup
 constexpr int LDS_SDFT_OFF = LDS_SDF;
 constexpr int LDS_DWS_OFF = LDS_SDF + MLI_SDF_T_PACK_BYTES;
-constexpr int LDS_SDF_BWD = LDS_DWS_OFF + MLP_WAVES * 260 * 4;  // one dW/db slice per wave
+constexpr int LDS_SDF_BWD = LDS_DWS_OFF + BWD_WAVES * 260 * 4;  // one dW/db slice per wave
 
 // Per sample: d sdf_i of the 5 points, then per point: layer 0 recomputed from the FIELD
 // encoding (as field_mlp_kernel), dZ0 = (w_sdf ds_i [+ W1^T dZ1 for the center]) *
@@ -650,7 +574,7 @@ constexpr int LDS_SDF_BWD = LDS_DWS_OFF + MLP_WAVES * 260 * 4;  // one dW/db sli
 // wave's own LDS slice (plain adds: distinct lanes, distinct addresses), then the slices in
 // wave order into the workgroup's partial row and sdf_bwd_reduce_kernel over the workgroups in
 // order: no atomics, bit-reproducible.
-__global__ __launch_bounds__(MLP_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_args a) {
+__global__ __launch_bounds__(BWD_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   load_block(lds, a.wsdf, PIECES);
   load_block(lds + LDS_SDFT_OFF, a.wsdf_t, SDFT_PIECES);
@@ -665,7 +589,7 @@ __global__ __launch_bounds__(MLP_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_arg
   const int tiles = S / 32;
   const float inv_scale = 1.0f / a.grad_scale;
   const float inv_rn = 1.0f / (float)S;
-  for (int tile = blockIdx.x * MLP_WAVES + wave; tile < tiles; tile += gridDim.x * MLP_WAVES) {
+  for (int tile = blockIdx.x * BWD_WAVES + wave; tile < tiles; tile += gridDim.x * BWD_WAVES) {
     const uint8_t* lds_t = lds + opaque_v(0);
     const int m = tile * 32 + c;
     const int r = m / a.N, k = m - r * a.N;
@@ -761,9 +685,14 @@ __global__ __launch_bounds__(MLP_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_arg
         load_rowc(lt, 1, t, h, wx);
         load_rowc(lt, 2, t, h, wy);
         load_rowc(lt, 3, t, h, wz);
-        f32x16 acc;
+        f32x16 acc;  // layer 0 recomputed exactly as the forward (sdf_from_enc)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc[i] = b0[i] + (wx[i] * px + wy[i] * py + wz[i] * pz);
+        for (int i = 0; i < 16; i += 2) {
+          const f32x2 v = pterm_x2((f32x2){b0[i], b0[i + 1]}, (f32x2){wx[i], wx[i + 1]}, (f32x2){wy[i], wy[i + 1]},
+                                   (f32x2){wz[i], wz[i + 1]}, px, py, pz);
+          acc[i] = v.x;
+          acc[i + 1] = v.y;
+        }
         const half8* frag = reinterpret_cast<const half8*>(lt + t * 8 * 1024) + lane;
 #pragma unroll
         for (int qq = 0; qq < 8; ++qq) acc = mfma32(frag[qq * 64], E[qq], acc);
@@ -813,18 +742,30 @@ __global__ __launch_bounds__(MLP_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_arg
   for (int i = threadIdx.x; i < 257; i += blockDim.x) {
     float v = 0.f;
 #pragma unroll
-    for (int w = 0; w < MLP_WAVES; ++w) v += dws_all[w * 260 + i];
+    for (int w = 0; w < BWD_WAVES; ++w) v += dws_all[w * 260 + i];
     a.partials[(size_t)blockIdx.x * 257 + i] = v;
   }
 }
 
-__global__ __launch_bounds__(320) void sdf_bwd_reduce_kernel(mli_sdf_bwd_args a, int blocks) {
-  const int i = threadIdx.x;
-  if (i >= 257) return;
+// One workgroup per output (256 dW + db): strided partial sums, then an LDS tree -- a fixed
+// order, so bit-reproducible (one thread looping over the 1024 partials took 330 us: a chain
+// of dependent loads).
+__global__ __launch_bounds__(256) void sdf_bwd_reduce_kernel(mli_sdf_bwd_args a, int blocks) {
+  __shared__ float red[256];
+  const int i = blockIdx.x, t = threadIdx.x;
   float v = 0.f;
-  for (int b = 0; b < blocks; ++b) v += a.partials[(size_t)b * 257 + i];
-  if (i < 256) a.dw_sdf[i] = v;
-  else a.db_sdf[0] = v;
+  for (int b = t; b < blocks; b += 256) v += a.partials[(size_t)b * 257 + i];
+  red[t] = v;
+  __syncthreads();
+#pragma unroll
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) red[t] += red[t + w];
+    __syncthreads();
+  }
+  if (t == 0) {
+    if (i < 256) a.dw_sdf[i] = red[0];
+    else a.db_sdf[0] = red[0];
+  }
 }
 
 // Hash-grid backward, level-outer like encode5_kernel: lane (c, h) = sample c, level 2qq+h.
@@ -1157,7 +1098,8 @@ extern "C" int mli_sdf(const mli_sdf_args* a, mli_stream_t s) {
     hipLaunchKernelGGL(sdf_kernel, dim3(blocks), dim3(256), LDS_SDF, (hipStream_t)s, *a);
     MLI_LAUNCH_CHECK();
   }
-  if (a->enc == nullptr || a->h0 == nullptr || a->grad == nullptr) return (int)hipErrorInvalidValue;
+  if (a->h0 == nullptr || a->grad == nullptr) return (int)hipErrorInvalidValue;
+  if (a->enc == nullptr) return (int)hipErrorInvalidValue;
   // FIELD: phase A (encodings of the 5 points) then phase B (layer 0 + softplus + sdf head),
   // in chunks of tiles (a chunk's encodings: tiles x 40 KiB).  Measured at 4096 x 128 samples
   // with the geometry prefetched beside the heads: 1024 / 2048 / 4096 / 8192 /
@@ -1168,10 +1110,9 @@ extern "C" int mli_sdf(const mli_sdf_args* a, mli_stream_t s) {
   for (int t0 = 0; t0 < tiles; t0 += CHUNK_TILES) {
     const int t1 = t0 + CHUNK_TILES < tiles ? t0 + CHUNK_TILES : tiles;
     hipLaunchKernelGGL(encode5_kernel, dim3((t1 - t0 + 3) / 4), dim3(256), 0, (hipStream_t)s, *a, t0, t1);
-    int blocks = (t1 - t0 + MLP_WAVES - 1) / MLP_WAVES;
+    int blocks = (t1 - t0 + 7) / 8;
     if (blocks > 512) blocks = 512;  // workgroups loop over the chunk's tiles (256 / 1024: DESIGN 9.0)
-    hipLaunchKernelGGL(field_mlp_kernel, dim3(blocks), dim3(MLP_WAVES * 64), LDS_SDF, (hipStream_t)s,
-                       *a, t0, t1);
+    hipLaunchKernelGGL(field_mlp_kernel<8>, dim3(blocks), dim3(8 * 64), LDS_SDF, (hipStream_t)s, *a, t0, t1);
     const int e = (int)hipGetLastError();
     if (e) return e;
   }
@@ -1211,8 +1152,8 @@ extern "C" int mli_sdf_bwd(const mli_sdf_bwd_args* a, mli_stream_t s) {
     return (int)hipErrorInvalidValue;
   if (!a->partials) return (int)hipErrorInvalidValue;
   const int blocks = sdf_bwd_blocks(S);
-  hipLaunchKernelGGL(sdf_bwd_kernel, dim3(blocks), dim3(MLP_WAVES * 64), LDS_SDF_BWD, (hipStream_t)s, *a);
-  hipLaunchKernelGGL(sdf_bwd_reduce_kernel, dim3(1), dim3(320), 0, (hipStream_t)s, *a, blocks);
+  hipLaunchKernelGGL(sdf_bwd_kernel, dim3(blocks), dim3(BWD_WAVES * 64), LDS_SDF_BWD, (hipStream_t)s, *a);
+  hipLaunchKernelGGL(sdf_bwd_reduce_kernel, dim3(257), dim3(256), 0, (hipStream_t)s, *a, blocks);
   MLI_LAUNCH_CHECK();
 }
 

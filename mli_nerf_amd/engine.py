@@ -206,6 +206,7 @@ class RenderEngine:
         R = rays["center"].shape[0]
         enc = None
         if mode == 1:
+            # the FIELD encoding image (stage a's backward re-reads it)
             tiles = (R * n_per_ray + 31) // 32
             enc = self._buf("enc5", (tiles * 32 * 640,), torch.float16)
         L.call("mli_sdf", L.SdfArgs(mode, R, n_per_ray, L.ptr(rays["center"]), L.ptr(rays["ray_unit"]),
@@ -213,6 +214,7 @@ class RenderEngine:
                                     L.ptr(self.wsdf), self.eps, self.grad_den, self.hess_den,
                                     self.cfg.outside_val, 1 if hess is not None else 0, L.ptr(out),
                                     L.ptr(grad), L.ptr(hess), L.ptr(h0), L.ptr(enc), int(self.active_levels)))
+        return enc
 
     @torch.no_grad()
     def sample(self, rays, u=None):
@@ -258,8 +260,8 @@ class RenderEngine:
         grad = self._buf("grad", (N, R, 3))
         hess = self._buf("hess", (N, R, 3)) if training else None
         h0 = self._buf("h0", (S * 256,), torch.float16)
-        self._sdf(rays, dists, N, sdf, mode=1, grad=grad, hess=hess, h0=h0)
-        return dict(sdf=sdf, grad=grad, hess=hess, h0=h0, enc=self._bufs["enc5"])
+        enc = self._sdf(rays, dists, N, sdf, mode=1, grad=grad, hess=hess, h0=h0)
+        return dict(sdf=sdf, grad=grad, hess=hess, h0=h0, enc=enc)
 
     def pq_mode(self, N, training):
         """The heads run in PQ mode (mli_rgb_fwd weights / q4, mli_dw4) for this render."""
