@@ -44,7 +44,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mli_stream_t; /* == hipStream_t */
 
-#define MLI_ABI_VERSION 12
+#define MLI_ABI_VERSION 13
 #define MLI_HIDDEN 256
 #define MLI_LEVELS 16
 #define MLI_LEVEL_FEAT 8
@@ -375,7 +375,7 @@ typedef struct {
   float w_eikonal, w_curvature;  /* loss weights / (R*N) are applied in-kernel */
   float grad_scale;
   float* d_enc;           /* [S/32][5][8][64][8] fp32 (unscaled) */
-  uint16_t* dz0_frag;     /* [5][S/32][16][64][8] scaled dZ0 of the 5 points (ACC order) */
+  uint16_t* dz0_rows;     /* [256][5S] fp16 scaled dZ0 of the 5 points, column pi*S + m (wgrad rows) */
   uint16_t* x0_rows;      /* [131][5S] fp16 layer-0 input rows (p 0..2, enc 3..130); this writes rows 0..2 */
   float* dw_sdf;          /* [256] scaled (written) */
   float* db_sdf;          /* [1] scaled (written) */
@@ -384,7 +384,7 @@ typedef struct {
   float* partials;        /* scratch [workgroups][257] */
 } mli_sdf_bwd_args;
 int mli_sdf_bwd(const mli_sdf_bwd_args* a, mli_stream_t s);
-/* bytes[0..3]: d_enc, dz0_frag, x0_rows, partials. */
+/* bytes[0..3]: d_enc, dz0_rows, x0_rows, partials. */
 int mli_sdf_bwd_workspace(const mli_sdf_bwd_args* a, int64_t* bytes);
 
 /* W0_enc^T fragments (A operand of d enc = W0_enc^T dZ0; rows ordered so each lane half
@@ -401,7 +401,11 @@ int mli_pack_sdf_t(const mli_pack_sdf_t_args* a, mli_stream_t s);
  * corner feature), levels < active_levels.  Default: fp32 atomics into the caller-zeroed
  * d_table.  deterministic: the run totals are added as fixed-point int64 (2^-40 units) into
  * the caller-zeroed workspace -- integer sums do not depend on their order -- and a second
- * launch writes d_table = float(sum * 2^-40) (overwritten): bit-reproducible. */
+ * launch writes d_table = float(sum * 2^-40) (overwritten): bit-reproducible.  The fixed point
+ * quantizes as well as reorders: every added run total is rounded to the nearest 2^-40
+ * (9.1e-13), so an element of n contributions is within n * 2^-41 of the exact sum before its
+ * final float rounding, run totals below 4.5e-13 vanish, and |sum| must stay below 2^23.
+ * The workspace is 8 B per table element (2.9 GB at 2^22 entries per level). */
 typedef struct {
   int R, N;
   const float* center; const float* ray_unit; const float* dists;

@@ -284,6 +284,9 @@ class RenderEngine:
         mode: the composite weights first, then the heads with the output-layer partials."""
         N, R = dists.shape
         S = N * R
+        if S % 256:
+            raise ValueError("heads: rays x samples = %d x %d is not a whole number of 256-sample tiles (the "
+                             "reference configs' batches are: 4096 / 8192 rays x 128 / 192 samples)" % (R, N))
         nh = len(self.head_specs)
         y = self._buf("y", (N, R, 8))
         if nh == 1:
@@ -640,13 +643,12 @@ class RenderEngine:
                                            L.ptr(b["dzT"]), L.ptr(b["dz4T"]), L.ptr(d_nrm), L.ptr(b["dz1T"]),
                                            L.ptr(dh0)))
         d_enc = self._buf("d_enc", (S * 640,))
-        dz0f = self._buf("dz0_frag", (5 * S * 256,), f16)
         part = self._buf("sdf_bwd_part", (L.workspace("mli_sdf_bwd", L.SdfBwdArgs(R, N))[3] // 4,))
         L.call("mli_sdf_bwd", L.SdfBwdArgs(
             R, N, L.ptr(rays["center"]), L.ptr(rays["ray_unit"]), L.ptr(dists), L.ptr(rays["outside"]),
             L.ptr(fld["grad"]), L.ptr(fld["hess"]), L.ptr(d_sdf), L.ptr(d_grad), L.ptr(d_nrm), L.ptr(dh0),
             L.ptr(fld["enc"]), L.ptr(self.wsdf), L.ptr(self.wsdf_t), self.eps, self.grad_den, self.hess_den,
-            float(w_eikonal), float(w_curvature), scale, L.ptr(d_enc), L.ptr(dz0f), L.ptr(b["x0_rows"]),
+            float(w_eikonal), float(w_curvature), scale, L.ptr(d_enc), L.ptr(b["dz0_rows"]), L.ptr(b["x0_rows"]),
             L.ptr(b["dws"][:256]), L.ptr(b["dws"][256:]), L.ptr(d_grad_ext), L.ptr(d_hess_ext), L.ptr(part)))
         det = 1 if self.deterministic else 0
         hws = None
@@ -654,6 +656,7 @@ class RenderEngine:
             hws = self._buf("hash_ws", (grad_table.numel(),), torch.int64)
             hws.zero_()
         else:
+            self._bufs.pop("hash_ws", None)  # 8 B per table element (2.9 GB at 2^22): freed outside det mode
             grad_table.zero_()
         L.call("mli_hash_bwd", L.HashBwdArgs(R, N, L.ptr(rays["center"]), L.ptr(rays["ray_unit"]), L.ptr(dists),
                                              L.ptr(d_enc), self.levels, self.eps, int(self.active_levels),
@@ -663,7 +666,6 @@ class RenderEngine:
         for pi in range(5):
             L.call("mli_frag_rows", L.FragRowsArgs(L.ptr(fld["enc"]) + pi * 8 * 512 * 2, 5 * 8 * 512, T, 8, 0,
                                                    L.ptr(b["x0_rows"]), 5 * S, pi * S, 3))
-        L.call("mli_frag_rows", L.FragRowsArgs(L.ptr(dz0f), 16 * 512, 5 * T, 16, 1, L.ptr(b["dz0_rows"]), 5 * S, 0, 0))
         dw_total = sum(m * k + m for m, k in [(256, layout.K0), (256, 256), (256, 256), (256, 256), (3, 256),
                                               (256, 256), (256, layout.SDF_K0)])
         b["dw"] = self._buf("dw_a", (dw_total,))

@@ -83,4 +83,12 @@ def test_stage_a_backward_bit_identical():
     assert t1.abs().sum() > 0
     g3, t3 = _grads_a(False)
     assert float((t1 - t3).norm() / t3.norm()) < 1e-5
+    # element-wise: the fixed point rounds each run total to 2^-40 (mli_hip.h, mli_hash_bwd_args),
+    # the fp32 atomics round each add to 2^-24 relative -- small entries stay within the quanta
+    err = (t1 - t3).abs()
+    small = (t3 != 0) & (t3.abs() < 1e-7)
+    print("table grad: %d small entries, max err %.3g; overall max rel %.3g" % (
+        int(small.sum()), float(err[small].max()) if small.any() else 0.0,
+        float((err / t3.abs().clamp_min(1e-30))[t3.abs() > 1e-7].max())))
+    assert (err <= t3.abs() * 1e-5 + 2.0 ** -28).all()
     assert float(torch.nn.functional.cosine_similarity(g1, g3, dim=0)) > 0.99999
