@@ -576,8 +576,10 @@ static_assert(LDS_SDF_BWD <= 160 * 1024, "sdf_bwd LDS");
 // LDS block as [32 samples][32 features] (8 B chunks XOR-swizzled by sample: conflict-free b64
 // writes and transposed reads, as mlp.hip q4_tile), then ds_read_b64_tr_b16: lane i of 16-lane
 // group g gets feature 16k + i of samples 8g .. 8g + 7 -- one 16 B store per lane and k.
-MLI_FI void dz0_rows_tile(uint8_t* xr, const half8& z0, const half8& z1, uint16_t* __restrict__ dst, size_t ld,
+MLI_FI void dz0_rows_tile(uint8_t* xr, const half8& z0, const half8& z1, uint16_t* __restrict__ ldst, size_t kstride,
                           int lane) {
+  // ldst: this lane's store address for k = 0 (row (lane & 15), column 8 (lane >> 4) of the
+  // tile); k = 1 is kstride (16 rows) further
   const int c = lane & 31, h = lane >> 5;
   // fragment element j of k-step u is feature 16u + 8(j >> 2) + 4h + (j & 3) -> 8 B chunk 4u + 2(j >> 2) + h
 #pragma unroll
@@ -590,7 +592,7 @@ MLI_FI void dz0_rows_tile(uint8_t* xr, const half8& z0, const half8& z1, uint16_
     }
   }
   asm volatile("" ::: "memory");
-  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3, i = lane & 15;
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int s0 = 8 * g + q, s1 = s0 + 4, chunk = 4 * k + p;
@@ -599,7 +601,7 @@ MLI_FI void dz0_rows_tile(uint8_t* xr, const half8& z0, const half8& z1, uint16_
     half8 v;
     v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
     v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-    __builtin_nontemporal_store(v, reinterpret_cast<half8*>(dst + (size_t)(16 * k + i) * ld + 8 * g));
+    __builtin_nontemporal_store(v, reinterpret_cast<half8*>(ldst + k * kstride));
   }
   asm volatile("" ::: "memory");  // the next tile's writes stay behind these reads
 }
@@ -713,45 +715,57 @@ __global__ __launch_bounds__(BWD_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_arg
 #pragma unroll
         for (int i = 0; i < 16; ++i) de[u][i] = 0.f;
       const size_t ld5 = (size_t)TAPS * S;
-      uint16_t* zrows = a.dz0_rows + (size_t)pi * S + (size_t)tile * 32;  // column pi * S + m of [256][5S]
+      // column pi * S + m of [256][5S]: this lane's store address (row lane & 15, columns 8 (lane >> 4) ..)
+      uint16_t* zlane = a.dz0_rows + (size_t)pi * S + (size_t)tile * 32 + (size_t)(lane & 15) * ld5 + 8 * (lane >> 4);
       uint8_t* xr = lds + LDS_ROWS_OFF + wave * 2048;
 #pragma unroll 1
       for (int t = 0; t < 8; ++t) {
         const uint8_t* lt = lds + opaque_v(0);
-        float b0[16], wx[16], wy[16], wz[16], ws[16];
-        load_rowc(lt, 0, t, h, b0);
-        load_rowc(lt, 1, t, h, wx);
-        load_rowc(lt, 2, t, h, wy);
-        load_rowc(lt, 3, t, h, wz);
-        f32x16 acc;  // layer 0 recomputed exactly as the forward (sdf_from_enc)
+        // layer 0 recomputed exactly as the forward (sdf_from_enc: row constants four at a time)
+        const f32x4* rc = reinterpret_cast<const f32x4*>(lt + ROWC_OFF + (t * 2 + h) * 64);
+        constexpr int A4 = ROWC_ARRAY / 16;  // f32x4 per array
+        f32x16 acc;
 #pragma unroll
-        for (int i = 0; i < 16; i += 2) {
-          const f32x2 v = pterm_x2((f32x2){b0[i], b0[i + 1]}, (f32x2){wx[i], wx[i + 1]}, (f32x2){wy[i], wy[i + 1]},
-                                   (f32x2){wz[i], wz[i + 1]}, px, py, pz);
-          acc[i] = v.x;
-          acc[i + 1] = v.y;
+        for (int u = 0; u < 4; ++u) {
+          const f32x4 b0 = rc[u], wx = rc[A4 + u], wy = rc[2 * A4 + u], wz = rc[3 * A4 + u];
+#pragma unroll
+          for (int j = 0; j < 4; j += 2) {
+            const f32x2 v = pterm_x2((f32x2){b0[j], b0[j + 1]}, (f32x2){wx[j], wx[j + 1]},
+                                     (f32x2){wy[j], wy[j + 1]}, (f32x2){wz[j], wz[j + 1]}, px, py, pz);
+            acc[4 * u + j] = v.x;
+            acc[4 * u + j + 1] = v.y;
+          }
         }
         const half8* frag = reinterpret_cast<const half8*>(lt + t * 8 * 1024) + lane;
 #pragma unroll
         for (int qq = 0; qq < 8; ++qq) acc = mfma32(frag[qq * 64], E[qq], acc);
-        load_rowc(lt, 4, t, h, ws);
         half8 c0, c1;
         if (pi == 0) { c0 = dh0p[(2 * t) * 64]; c1 = dh0p[(2 * t + 1) * 64]; }
         f32x16 dz;
         float part[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          // torch softplus backward: z = e^{beta x}; beta x > 20 ? 1 : z / (z + 1)
-          const float tt = acc[i] * 100.0f;
-          const float e = __builtin_amdgcn_exp2f(tt * 1.4426950408889634f);
-          const float dsig = tt > 20.0f ? 1.0f : e / (e + 1.0f);
-          float dh = ws[i] * dsp;
-          if (pi == 0) dh += (float)((i < 8) ? c0[i] : c1[i - 8]);
-          dz[i] = dh * dsig;
-          part[i] = dsp * softplus100(acc[i]);
+        for (int u = 0; u < 4; ++u) {
+          const f32x4 ws = rc[4 * A4 + u];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int i = 4 * u + j;
+            // one exp for softplus and its derivative: with q = e^{-|100 x|} (base 2, as
+            // softplus100), softplus = max(x, 0) + log(1 + q) / 100 (bit-identical to
+            // softplus100) and torch's backward sigmoid(100 x) = 1 / (1 + q) for x >= 0, else
+            // q / (1 + q) (within an ulp of its z / (z + 1), without the overflow guard)
+            const float x = acc[i];
+            const float q = __builtin_amdgcn_exp2f(-fabsf(x * 144.26950408889634f));
+            const float r = __builtin_amdgcn_rcpf(1.0f + q);
+            const float dsig = x >= 0.0f ? r : q * r;
+            const float sp = fmaf(__builtin_amdgcn_logf(q + 1.0f), 0.0069314718055994531f, relu_f(x));
+            float dh = ws[j] * dsp;
+            if (pi == 0) dh += (float)((i < 8) ? c0[i] : c1[i - 8]);
+            dz[i] = dh * dsig;
+            part[i] = dsp * sp;
+          }
         }
         const half8 z0 = acc_to_frag(dz, 0), z1 = acc_to_frag(dz, 1);
-        dz0_rows_tile(xr, z0, z1, zrows + (size_t)(32 * t) * ld5, ld5, lane);
+        dz0_rows_tile(xr, z0, z1, zlane + (size_t)(32 * t) * ld5, 16 * ld5, lane);
         const half8* fr = reinterpret_cast<const half8*>(lt + LDS_SDFT_OFF + (2 * t) * 1024) + lane;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
