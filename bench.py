@@ -364,6 +364,29 @@ class HipPlatform:
 
 
 PLATFORM = HipPlatform()
+
+
+def cu_mask_stream(dev, spec):
+    """Experiment: a stream whose kernels run only on a CU subset (hipExtStreamCreateWithCUMask),
+    wrapped as a torch ExternalStream.  spec: every:K (CU ids i % K == 0), skip:K (the rest),
+    first:K (ids 0..K-1)."""
+    import ctypes
+    kind, k = spec.split(":")
+    k = int(k)
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    sel = {"every": lambda i: i % k == 0, "skip": lambda i: i % k != 0, "first": lambda i: i < k}[kind]
+    words = [0] * ((ncu + 31) // 32)
+    for i in range(ncu):
+        if sel(i):
+            words[i // 32] |= 1 << (i % 32)
+    hip = ctypes.CDLL("libamdhip64.so")
+    s = ctypes.c_void_p()
+    arr = (ctypes.c_uint32 * len(words))(*words)
+    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(s), ctypes.c_uint32(len(words)), arr)
+    if rc != 0:
+        raise RuntimeError("hipExtStreamCreateWithCUMask: %d" % rc)
+    progress("stream %s: %d of %d CUs" % (spec, sum(bin(w).count("1") for w in words), ncu))
+    return torch.cuda.ExternalStream(s.value, device=dev)
 WORKER_SCRIPT = None   # the rank program --gpus N spawns (default: this file)
 
 
@@ -441,6 +464,10 @@ def main(argv=None):
     ap.add_argument("--priority", choices=("none", "main", "side"), default="none",
                     help="pipeline: run the step on a high-priority stream (main) or give the prefetch "
                          "stream the high priority (side)")
+    ap.add_argument("--side-cus", default=None,
+                    help="pipeline experiment: restrict the prefetch stream to a CU subset "
+                         "(hipExtStreamCreateWithCUMask): every:K = CUs i %% K == 0, first:K, skip:K = the complement of every:K")
+    ap.add_argument("--main-cus", default=None, help="pipeline experiment: the same for the step's stream")
     ap.add_argument("--tail", choices=("fused", "three"), default="fused",
                     help="stage-b training tail: fused (mli_composite_loss, one launch) or the three calls "
                          "mli_composite_fwd / mli_stage_b_loss / mli_composite_bwd")
@@ -539,6 +566,10 @@ def main(argv=None):
     if args.priority == "side":
         trainer.side_priority = hi
     main_stream = torch.cuda.Stream(device=dev, priority=hi) if args.priority == "main" else None
+    if args.side_cus:
+        trainer._side = cu_mask_stream(dev, args.side_cus)
+    if args.main_cus:
+        main_stream = cu_mask_stream(dev, args.main_cus)
     if main_stream is not None:
         torch.cuda.synchronize()
         torch.cuda.set_stream(main_stream)
