@@ -20,7 +20,10 @@
 //    + feature-major activation stores for the weight gradients in training), sigmoid
 //    for the outputs.  Feature-major tiles are transposed through LDS so each 256-sample
 //    row leaves as 512 contiguous bytes.
+#pragma once
 #include "common.h"
+
+#include <type_traits>
 
 namespace {
 
@@ -43,9 +46,10 @@ enum Role { ALL = 0, DMA = 1, STORE = 2 };
 // The ring DMA of one chunk is ND waves x RND pieces of 1 KiB (16 B per lane); the
 // feature-major staging tile is [32 features][NW * 32 samples] fp16, double buffered; the
 // backward's ReLU-mask blocks are NW tiles x 1 KiB, double buffered.
-template <int NW_, int MAXP, bool SPLIT_>
+template <int NW_, int MAXP, bool SPLIT_, int PF_ = 0>
 struct Geo {
   static constexpr int NW = NW_;
+  static constexpr int PF = PF_;  // weight-fragment read depth of chunk_mma
   static constexpr bool SPLIT = SPLIT_;
   static constexpr int THREADS = NW * 64;
   static constexpr int SAMPLES = NW * 32;
@@ -181,8 +185,13 @@ MLI_FI void stage_flush(Stager& sg, const uint8_t* lds, int S) {
 MLI_FI float relu1(float x) {
   return __builtin_bit_cast(float, max(__builtin_bit_cast(int, x), 0));
 }
-// acc = W_chunk (32 x 16*KS) * X (16*KS x 32) + bias
-template <int KS>
+// acc = W_chunk (32 x 16*KS) * X (16*KS x 32) + bias.  PF = 0: the compiler's schedule (it reads
+// two weight fragments ahead and waits lgkmcnt(0) before every MFMA pair, so each pair pays the
+// LDS latency); PF > 0: the fragments are read PF ahead, one read issued after each MFMA (the
+// order pinned by sched_group_barrier).  Measured (profiles/r3/pf): PF = 4 takes the training
+// heads forward 1.19 -> 1.15 ms and rgb_bwd 0.885 -> 0.86 ms; the eval forward is slower with
+// it (3.85 -> 3.95 ms per 20000-ray chunk), so it keeps PF = 0.
+template <int KS, int PF = 0>
 MLI_FI f32x16 chunk_mma(const uint8_t* chunk, const half8* X, int lane) {
   const int h = lane >> 5;
   f32x16 acc;
@@ -193,8 +202,28 @@ MLI_FI f32x16 chunk_mma(const uint8_t* chunk, const half8* X, int lane) {
     acc[4 * u] = b[0]; acc[4 * u + 1] = b[1]; acc[4 * u + 2] = b[2]; acc[4 * u + 3] = b[3];
   }
   const half8* w = reinterpret_cast<const half8*>(chunk) + lane;
+  if constexpr (PF == 0) {
 #pragma unroll
-  for (int q = 0; q < KS; ++q) acc = mfma32(w[q * 64], X[q], acc);
+    for (int q = 0; q < KS; ++q) acc = mfma32(w[q * 64], X[q], acc);
+  } else {
+    constexpr int D = PF < KS ? PF : KS;
+    half8 wr[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) wr[q] = w[q * 64];
+#pragma unroll
+    for (int q = 0; q < KS; ++q) {
+      acc = mfma32(wr[q % D], X[q], acc);
+      if (q + D < KS) wr[q % D] = w[(q + D) * 64];
+    }
+    // the pipeline: D reads, then (MFMA, read) pairs, then the last D MFMAs
+#pragma unroll
+    for (int q = 0; q < D; ++q) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+#pragma unroll
+    for (int q = 0; q < KS; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      if (q + D < KS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+  }
   return acc;
 }
 
@@ -223,7 +252,7 @@ MLI_FI void run_layer(Ring& rg, uint8_t* lds, Stager& sg, int S, const half8* X,
         stage_flush<G, ROLE>(sg, lds, S);
       }
     }
-    const f32x16 acc = chunk_mma<KS>(lds + (rg.cur % NSLOT) * G::SLOT, X, lane);
+    const f32x16 acc = chunk_mma<KS, G::PF>(lds + (rg.cur % NSLOT) * G::SLOT, X, lane);
     epi(t, acc);
     // retire chunk cur+1 (its DMAs went out DIST-1 phases ago): every VMEM op issued after
     // them may stay in flight -- the weight DMAs of the DIST-1 later phases, the mask DMAs
@@ -514,16 +543,18 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
 // beside the other's epilogue): training forward 1.37 vs 1.29 ms, eval 0.88 vs 0.80 ms, rgb_bwd
 // 0.86 vs 0.81 ms -- the weight chunks stream through LDS once per workgroup, so halving the
 // workgroup doubles the ring DMA and LDS-write work per sample.
-typedef Geo<8, 20, true> GFwd;
-typedef Geo<8, 17, true> GBwd;
+typedef Geo<8, 20, true> GFwd;      // eval forward
+typedef Geo<8, 20, true, 4> GFwdT;  // training forward (same layout, PF 4)
+typedef Geo<8, 17, true, 4> GBwd;
 
 // the first / second half of the waves take the DMA / STORE roles (see Role), compiled as two
 // programs
 template <bool TRAIN, bool PQ>
 __global__ __launch_bounds__(GFwd::THREADS) void rgb_fwd_kernel(mli_rgb_fwd_args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= GFwd::NW / 2) rgb_fwd_body<GFwd, TRAIN, PQ, STORE>(a, lds);
-  else rgb_fwd_body<GFwd, TRAIN, PQ, DMA>(a, lds);
+  typedef typename std::conditional<TRAIN, GFwdT, GFwd>::type G;
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= G::NW / 2) rgb_fwd_body<G, TRAIN, PQ, STORE>(a, lds);
+  else rgb_fwd_body<G, TRAIN, PQ, DMA>(a, lds);
 }
 
 // ---------------------------------------------------------------------- backward dX chain
@@ -624,221 +655,9 @@ MLI_FI void rgb_bwd_body(const mli_rgb_bwd_args& a, uint8_t* lds) {
   vm_wait(0);
 }
 
-__global__ __launch_bounds__(GBwd::THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= GBwd::NW / 2) rgb_bwd_body<GBwd, STORE>(a, lds);
-  else rgb_bwd_body<GBwd, DMA>(a, lds);
-}
-
-
-// ---------------------------------------------------------------------- stage a: geometry dX chain
-// The single 'rgb' head (NeuralLumen/utils/modules.py:164-174) backward down to its inputs,
-// then SDF layer 1.  Chunks: W4^T (8 x KS 1), W3^T, W2^T, W1^T (24 x KS 16), W0^T (9 n-tiles
-// over packed input rows 0..287: feat (ACC order) + the p/normal k-step), W1sdf^T (8 x KS 16).
-MLI_FI int geo_bytes(int c) { return c < 8 ? CH(1) : CH(16); }
-constexpr int GEO_CHUNKS = 8 + 24 + 9 + 8;
-
-typedef Geo<8, 17, false> GGeo;
-
-__global__ __launch_bounds__(GGeo::THREADS) void geo_bwd_kernel(mli_geo_bwd_args a) {
-  typedef GGeo G;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = lane & 31, h = lane >> 5;
-  const int S = a.R * a.N;
-  const int tiles = S / 32;
-  const int tile = blockIdx.x * G::NW + wave;
-  const int m = tile * 32 + c;
-  const int r = m / a.N, k = m - r * a.N;
-  const size_t slot = (size_t)k * a.R + r;
-  auto bytes = [](int cc) MLI_LAMBDA_FI { return geo_bytes(cc); };
-  // ReLU-mask block of head layer 3 - L (L = 0..3), one 16 B DMA per thread into slot L & 1
-  auto mask_dma = [&](int L) MLI_LAMBDA_FI {
-    const int ml = 3 - min(L, 3);
-    const uint8_t* src = reinterpret_cast<const uint8_t*>(a.masks) +
-                         (((size_t)ml * tiles + (size_t)blockIdx.x * G::NW) * 64) * 16;
-    glds16(src + threadIdx.x * 16, lds + G::MASK_OFF + (L & 1) * G::MASKB + wave * 1024);
-  };
-
-  Ring rg;
-  ring_start(rg, a.wgeo, GEO_CHUNKS, bytes);
-  mask_dma(0);
-#pragma unroll
-  for (int d = 0; d < DIST; ++d) ring_issue<G, ALL>(rg, lds, bytes);
-  vm_wait((DIST - 1) * G::template ring_ops<ALL>());
-  block_sync();
-
-  half8 A[16], B[16];
-  Stager sg{nullptr, 0, 0};
-  const size_t col0 = (size_t)blockIdx.x * G::SAMPLES;
-  half8 z4;
-  {
-    const float* dz = a.dz4 + 8 * slot;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) z4[j] = (f16)0.f;
-    if (h == 0) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const f16 zj = (f16)dz[j];
-        z4[j] = zj;
-        a.dz4T[(size_t)j * S + m] = __builtin_bit_cast(uint16_t, zj);
-      }
-    }
-  }
-  struct MaskPre {
-    decltype(mask_dma)& dma;
-    int next_layer;
-    MLI_FI int count(int t) const { return t == 8 - DIST ? 1 : 0; }
-    MLI_FI void issue(int t) const {
-      if (t == 8 - DIST) dma(next_layer);
-    }
-  };
-  auto pre = [&](int li) MLI_LAMBDA_FI { return MaskPre{mask_dma, li + 1}; };
-  auto mask_epi = [&](half8* out, int layer, int li) MLI_LAMBDA_FI {
-    return [&, out, layer, li](int t, const f32x16& acc) MLI_LAMBDA_FI {
-      const u32x4 mv =
-          *reinterpret_cast<const u32x4*>(lds + G::MASK_OFF + (li & 1) * G::MASKB + wave * 1024 + lane * 16);
-      const int wi = t >> 1;
-      const uint32_t word = wi == 0 ? mv[0] : wi == 1 ? mv[1] : wi == 2 ? mv[2] : mv[3];
-      const uint32_t bits = word >> ((t & 1) * 16);
-      f32x16 v;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = ((bits >> i) & 1u) ? acc[i] : 0.0f;
-      out[2 * t] = acc_to_frag(v, 0);
-      out[2 * t + 1] = acc_to_frag(v, 1);
-      stage_tile<G>(sg, lds, out[2 * t], out[2 * t + 1], a.dzT + ((size_t)layer * 256 + 32 * t) * S + col0, lane);
-    };
-  };
-  run_layer<G, ALL, 1, 8, true, 0, false>(rg, lds, sg, S, &z4, lane, bytes, pre(0), mask_epi(A, 3, 0));
-  run_layer<G, ALL, 16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, pre(1), mask_epi(B, 2, 1));
-  run_layer<G, ALL, 16, 8, true, 0, false>(rg, lds, sg, S, B, lane, bytes, pre(2), mask_epi(A, 1, 2));
-  run_layer<G, ALL, 16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, NoPre{}, mask_epi(B, 0, 3));
-  // feat frags (softplus output of SDF layer 1, forward scratch), one tile ahead of its use:
-  // tile 0 now, tile t+1 ahead of phase t's weight DMAs (counted as pre-issued VMEM ops)
-  const half8* fsrc = reinterpret_cast<const half8*>(a.feat_frag + (size_t)tile * FRAG_TILE) + lane;
-  half8 F[2][2];
-  F[0][0] = fsrc[0];
-  F[0][1] = fsrc[64];
-  struct FeatPre {
-    const half8* src;
-    half8 (&F)[2][2];
-    MLI_FI int count(int t) const { return t < 7 ? 2 : 0; }
-    MLI_FI void issue(int t) const {
-      if (t < 7) {
-        F[(t + 1) & 1][0] = src[(2 * t + 2) * 64];
-        F[(t + 1) & 1][1] = src[(2 * t + 3) * 64];
-      }
-    }
-  };
-  // dX0 = W0^T dZ0: tiles 0..7 = d feat -> dZ1sdf = d feat * softplus'(z1), with
-  // softplus'(z1) = 1 - exp(-100 feat) (torch: z/(z+1), z = e^{100 z1}; 1 past the threshold);
-  // tile 8 = rows 256..287 (p 256..258, normal 259..261: (i=3,h=0), (i=0,h=1), (i=1,h=1))
-  run_layer<G, ALL, 16, 9, true, 0, false>(rg, lds, sg, S, B, lane, bytes, FeatPre{fsrc, F},
-                                   [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
-    if (t < 8) {
-      f32x16 v;
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float f = (float)F[t & 1][s2][j];
-          v[8 * s2 + j] = acc[8 * s2 + j] * (1.0f - __expf(-100.0f * f));
-        }
-      A[2 * t] = acc_to_frag(v, 0);
-      A[2 * t + 1] = acc_to_frag(v, 1);
-      stage_tile<G>(sg, lds, A[2 * t], A[2 * t + 1], a.dz1T + (size_t)(32 * t) * S + col0, lane);
-    } else {
-      float* dn = a.d_nrm + 4 * slot;
-      if (h == 0) {
-        dn[0] = acc[3];
-      } else {
-        dn[1] = acc[0];
-        dn[2] = acc[1];
-      }
-    }
-  });
-  // d h0 (layer-1 path) = W1sdf^T dZ1sdf -> frag image (ACC order, as the h0 image)
-  uint16_t* dtile = a.dh0_frag + (size_t)tile * FRAG_TILE;
-  run_layer<G, ALL, 16, 8, false, 2, false>(rg, lds, sg, S, A, lane, bytes, NoPre{},
-                                    [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
-    half8* dst = reinterpret_cast<half8*>(dtile) + (2 * t) * 64 + lane;
-    __builtin_nontemporal_store(acc_to_frag(acc, 0), dst);
-    __builtin_nontemporal_store(acc_to_frag(acc, 1), dst + 64);
-  });
-  vm_wait(0);
-}
-
 }  // namespace
 
-extern "C" int mli_rgb_fwd(const mli_rgb_fwd_args* a, mli_stream_t s) {
-  const int S = a->R * a->N;
-  if (S % 256 != 0) return (int)hipErrorInvalidValue;
-  const bool train = a->xT != nullptr;
-  if (train && (a->x0T == nullptr || a->masks == nullptr)) return (int)hipErrorInvalidValue;
-  if (a->n_heads != 1 && a->n_heads != 3) return (int)hipErrorInvalidValue;
-  // output-layer partials: training only, one ray per 32-sample tile, both pointers or none
-  const bool pq = a->weights != nullptr;
-  if (pq && (!train || a->q4 == nullptr || a->N % 32 != 0)) return (int)hipErrorInvalidValue;
-  if (!pq && a->q4 != nullptr) return (int)hipErrorInvalidValue;
-  const dim3 grid(S / GFwd::SAMPLES), block(GFwd::THREADS);
-  if (pq)
-    hipLaunchKernelGGL((rgb_fwd_kernel<true, true>), grid, block, GFwd::LDS_FWD_PQ, (hipStream_t)s, *a);
-  else if (train)
-    hipLaunchKernelGGL((rgb_fwd_kernel<true, false>), grid, block, GFwd::LDS_FWD, (hipStream_t)s, *a);
-  else
-    hipLaunchKernelGGL((rgb_fwd_kernel<false, false>), grid, block, GFwd::LDS_FWD, (hipStream_t)s, *a);
-  MLI_LAUNCH_CHECK();
-}
-
-extern "C" int mli_rgb_bwd(const mli_rgb_bwd_args* a, mli_stream_t s) {
-  const int S = a->R * a->N;
-  if (S % 256 != 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(rgb_bwd_kernel, dim3(S / GBwd::SAMPLES), dim3(GBwd::THREADS), GBwd::LDS_BWD, (hipStream_t)s,
-                     *a);
-  MLI_LAUNCH_CHECK();
-}
-
-extern "C" int mli_rgb_fwd_workspace(const mli_rgb_fwd_args* a, int64_t* bytes) {
-  const int64_t S = (int64_t)a->R * a->N;
-  if (S <= 0 || S % 256 != 0 || (a->n_heads != 1 && a->n_heads != 3)) return (int)hipErrorInvalidValue;
-  const bool pq = a->weights != nullptr;
-  if (pq && a->N % 32 != 0) return (int)hipErrorInvalidValue;
-  bytes[0] = S * 8 * 4;                                   // y
-  bytes[1] = S * 256 * 2;                                 // feat_frag
-  bytes[2] = (int64_t)MLI_HEAD_K0 * S * 2;                // x0T (training)
-  bytes[3] = (int64_t)a->n_heads * (pq ? 3 : 4) * 256 * S * 2;  // xT (training)
-  bytes[4] = (int64_t)a->n_heads * 4 * (S / 32) * 64 * 16;  // masks (training)
-  bytes[5] = pq ? (S / 256) * MLI_Q4_SEGS(a->N) * a->n_heads * 257 * 4 * 4 : 0;  // q4 (PQ)
-  return 0;
-}
-
-extern "C" int mli_rgb_bwd_workspace(const mli_rgb_bwd_args* a, int64_t* bytes) {
-  const int64_t S = (int64_t)a->R * a->N;
-  if (S <= 0 || S % 256 != 0) return (int)hipErrorInvalidValue;
-  bytes[0] = 3 * 4 * 256 * S * 2;  // dzT
-  bytes[1] = 3 * 4 * S * 2;        // dz4T
-  return 0;
-}
-
-extern "C" int mli_geo_bwd_workspace(const mli_geo_bwd_args* a, int64_t* bytes) {
-  const int64_t S = (int64_t)a->R * a->N;
-  if (S <= 0 || S % 256 != 0) return (int)hipErrorInvalidValue;
-  bytes[0] = 4 * 256 * S * 2;  // dzT
-  bytes[1] = 4 * S * 2;        // dz4T
-  bytes[2] = S * 4 * 4;        // d_nrm
-  bytes[3] = 256 * S * 2;      // dz1T
-  bytes[4] = S * 256 * 2;      // dh0_frag
-  bytes[5] = 0;
-  return 0;
-}
-
-extern "C" int mli_geo_bwd(const mli_geo_bwd_args* a, mli_stream_t s) {
-  const int S = a->R * a->N;
-  if (S % 256 != 0) return (int)hipErrorInvalidValue;
-  if (!a->dz4 || !a->wgeo || !a->masks || !a->feat_frag || !a->dzT || !a->dz4T || !a->d_nrm || !a->dz1T ||
-      !a->dh0_frag)
-    return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(geo_bwd_kernel, dim3(S / GGeo::SAMPLES), dim3(GGeo::THREADS), GGeo::LDS_BWD, (hipStream_t)s,
-                     *a);
-  MLI_LAUNCH_CHECK();
-}
+// launchers of the training forward (their kernels compile in their own translation units:
+// mlp_fwd_pq.hip, mlp_fwd_train.hip)
+__attribute__((visibility("hidden"))) int mli_launch_rgb_fwd_pq(const mli_rgb_fwd_args* a, hipStream_t s);
+__attribute__((visibility("hidden"))) int mli_launch_rgb_fwd_train(const mli_rgb_fwd_args* a, hipStream_t s);

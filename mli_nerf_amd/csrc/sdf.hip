@@ -574,7 +574,7 @@ static_assert(LDS_SDF_BWD <= 160 * 1024, "sdf_bwd LDS");
 // 2t+1) -> feature-major rows dst[f * ld + s] (the wgrad operand layout; before, a frag image
 // and a separate mli_frag_rows pass: 2.7 GB of traffic per stage-a step).  Through the wave's
 // LDS block as [32 samples][32 features] (8 B chunks XOR-swizzled by sample: conflict-free b64
-// writes and transposed reads, as mlp.hip q4_tile), then ds_read_b64_tr_b16: lane i of 16-lane
+// writes and transposed reads, as mlp_core.h q4_tile), then ds_read_b64_tr_b16: lane i of 16-lane
 // group g gets feature 16k + i of samples 8g .. 8g + 7 -- one 16 B store per lane and k.
 MLI_FI void dz0_rows_tile(uint8_t* xr, const half8& z0, const half8& z1, uint16_t* __restrict__ ldst, size_t kstride,
                           int lane) {
