@@ -185,16 +185,24 @@ __global__ __launch_bounds__(512) void wgrad_kernel(KArgs ka) {
 // (its second stage spills).  A stage is [BM + BN rows][BKD * 2 bytes], unpadded; 16 B chunk c
 // of row r sits at position c ^ ((r >> 2) & 3), so the 16 rows a ds_read_b128 lane group reads
 // cover all 64 banks.  One DMA wave-instruction fills 16 rows (lane l: row l / 4, position l % 4).
-constexpr int BKD = 32;
-constexpr int RBD = BKD * 2;  // bytes per row of a stage
-MLI_FI int swz(int r, int c) { return c ^ ((r >> 2) & 3); }
+// BKD samples per stage: CPR = BKD / 8 chunks of 16 B per row, 64 / CPR rows per DMA
+// wave-instruction; chunk c of row r sits at c ^ ((r / (16 / CPR)) & (CPR - 1)) (32 samples:
+// c ^ ((r >> 2) & 3); 64: c ^ ((r >> 1) & 7)), so each 16-lane group of a ds_read_b128 covers
+// all 64 banks.
+template <int BKD>
+MLI_FI int swz(int r, int c) {
+  constexpr int CPR = BKD / 8;
+  return c ^ ((r / (16 / CPR)) & (CPR - 1));
+}
 
-template <int BM, int BN, int WM, int WN, int NBUF, bool SHARE_B>
+template <int BM, int BN, int WM, int WN, int NBUF, bool SHARE_B, int BKD = 32>
 __global__ __launch_bounds__(512) void wgrad_dma_kernel(KArgs ka) {
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  constexpr int RBD = BKD * 2;  // bytes per row of a stage
+  constexpr int CPR = BKD / 8, RPI = 64 / CPR;  // 16 B chunks per row, rows per DMA instruction
   constexpr int ROWS = BM + BN, STAGE = ROWS * RBD;
-  constexpr int PIECES = ROWS / 16, PPW = (PIECES + 7) / 8;  // DMA wave-instructions per stage / wave
-  static_assert(ROWS % 16 == 0, "stage rows");
+  constexpr int PIECES = ROWS / RPI, PPW = (PIECES + 7) / 8;  // DMA wave-instructions per stage / wave
+  static_assert(ROWS % RPI == 0, "stage rows");
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   int bid = blockIdx.x;
   if (SHARE_B) {  // as wgrad_kernel
@@ -226,8 +234,8 @@ __global__ __launch_bounds__(512) void wgrad_dma_kernel(KArgs ka) {
 #pragma unroll
   for (int u = 0; u < PPW; ++u) {
     const int piece = min(u * 8 + wave, PIECES - 1);
-    const int row = piece * 16 + (lane >> 2), pos = lane & 3;
-    const int c = swz(row, pos);  // the chunk that belongs at this position
+    const int row = piece * RPI + lane / CPR, pos = lane % CPR;
+    const int c = swz<BKD>(row, pos);  // the chunk that belongs at this position
     const uint16_t* rp = row < BM ? J.a + (size_t)min(tm * BM + row, J.M - 1) * S
                                   : J.b + (size_t)min(tn * BN + row - BM, J.K - 1) * S;
     src[u] = rp + c * 8;
@@ -247,7 +255,7 @@ __global__ __launch_bounds__(512) void wgrad_dma_kernel(KArgs ka) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
   const bool do_bias = (J.db != nullptr) && tn == 0;
-  float bsum = 0.f;  // row (tid >> 1) of the A tile, chunks 2 (tid & 1), 2 (tid & 1) + 1
+  float bsum = 0.f;  // row (tid >> 1) of the A tile, chunks (CPR / 2) (tid & 1) ..
 
   const int n_st = (k1 - k0) / BKD;
 #pragma unroll
@@ -263,12 +271,12 @@ __global__ __launch_bounds__(512) void wgrad_dma_kernel(KArgs ka) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int r = wm * TM * 32 + i * 32 + rl;
-        fa[i] = *reinterpret_cast<const half8*>(sb + r * RBD + swz(r, 2 * ks + h) * 16);
+        fa[i] = *reinterpret_cast<const half8*>(sb + r * RBD + swz<BKD>(r, 2 * ks + h) * 16);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int r = BM + wn * TN * 32 + j * 32 + rl;
-        fb[j] = *reinterpret_cast<const half8*>(sb + r * RBD + swz(r, 2 * ks + h) * 16);
+        fb[j] = *reinterpret_cast<const half8*>(sb + r * RBD + swz<BKD>(r, 2 * ks + h) * 16);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -278,8 +286,8 @@ __global__ __launch_bounds__(512) void wgrad_dma_kernel(KArgs ka) {
     if (do_bias && (tid >> 1) < BM) {
       const int r = tid >> 1;
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const half8 v = *reinterpret_cast<const half8*>(sb + r * RBD + swz(r, 2 * (tid & 1) + u) * 16);
+      for (int u = 0; u < CPR / 2; ++u) {
+        const half8 v = *reinterpret_cast<const half8*>(sb + r * RBD + swz<BKD>(r, (CPR / 2) * (tid & 1) + u) * 16);
 #pragma unroll
         for (int e = 0; e < 8; ++e) bsum += (float)v[e];
       }
@@ -444,7 +452,12 @@ enum { CLS_BIG = 1, CLS_WIDE = 2, CLS_THIN = 4 };
 // (SHARE_B) and stream through the LDS-DMA ring (wgrad_dma_kernel) with this many stages
 // (register staging 0.425 ms, the ring 0.415 ms)
 constexpr bool WIDE_SHARE = true;
-constexpr int WIDE_DMA = 4;
+// (4 stages of 32 samples 0.413 ms, 2 stages of 64 samples -- 128 B row segments
+// -- 0.353 ms)
+constexpr int WIDE_DMA = 2, WIDE_BKD = 64;
+// BIG through the same ring, 2 stages of 64 samples: 0.898 -> 0.847 ms (register staging of 64
+// samples before; the ring at 32-sample stages -- 64 B row segments -- measured 0.998 ms)
+constexpr int BIG_DMA = 2;
 
 inline int job_class(const mli_wgrad_job& j) {
   return j.M <= 32 ? CLS_THIN : (j.K <= 256 ? CLS_BIG : CLS_WIDE);
@@ -494,7 +507,7 @@ int64_t plan(const mli_wgrad_args* a, int cls, KArgs& ka) {
   return floats;
 }
 
-template <int BM, int BN, int WM, int WN, int OCC, int DEPTH, bool SHARE_B = false, int DMA_NBUF = 0>
+template <int BM, int BN, int WM, int WN, int OCC, int DEPTH, bool SHARE_B = false, int DMA_NBUF = 0, int DMA_BKD = 32>
 int launch(const mli_wgrad_args* a, int cls, hipStream_t s) {
   KArgs ka;
   const int64_t floats = plan<BM, BN, OCC, SHARE_B>(a, cls, ka);
@@ -509,10 +522,13 @@ int launch(const mli_wgrad_args* a, int cls, hipStream_t s) {
   if (SHARE_B && ka.share) {
     grid = 8 * ka.n_jobs * ((ka.n_split + 7) / 8);
     if constexpr (SHARE_B && DMA_NBUF > 0)
-      hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, DMA_NBUF, true>), dim3(grid), dim3(512),
-                         DMA_NBUF * (BM + BN) * RBD, s, ka);
+      hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, DMA_NBUF, true, DMA_BKD>), dim3(grid), dim3(512),
+                         DMA_NBUF * (BM + BN) * DMA_BKD * 2, s, ka);
     else if constexpr (SHARE_B)
       hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, DEPTH, true>), dim3(grid), dim3(512), (BM + BN) * ROWB, s, ka);
+  } else if constexpr (DMA_NBUF > 0 && !SHARE_B) {
+    hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, DMA_NBUF, false, DMA_BKD>), dim3(grid), dim3(512),
+                       DMA_NBUF * (BM + BN) * DMA_BKD * 2, s, ka);
   } else {
     hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, DEPTH>), dim3(grid), dim3(512), (BM + BN) * ROWB, s, ka);
   }
@@ -539,8 +555,8 @@ int launch(const mli_wgrad_args* a, int cls, hipStream_t s) {
 extern "C" int mli_wgrad(const mli_wgrad_args* a, mli_stream_t s) {
   if (a->S <= 0 || a->S % BK != 0) return (int)hipErrorInvalidValue;
   int e = 0;
-  if (a->classes & CLS_BIG) e = launch<256, 256, 4, 2, 1, 2>(a, CLS_BIG, (hipStream_t)s);
-  if (!e && (a->classes & CLS_WIDE)) e = launch<256, 320, 4, 2, 1, 1, WIDE_SHARE, WIDE_DMA>(a, CLS_WIDE, (hipStream_t)s);
+  if (a->classes & CLS_BIG) e = launch<256, 256, 4, 2, 1, 2, false, BIG_DMA, 64>(a, CLS_BIG, (hipStream_t)s);
+  if (!e && (a->classes & CLS_WIDE)) e = launch<256, 320, 4, 2, 1, 1, WIDE_SHARE, WIDE_DMA, WIDE_BKD>(a, CLS_WIDE, (hipStream_t)s);
   if (!e && (a->classes & CLS_THIN)) e = launch<32, 256, 1, 8, 2, 2>(a, CLS_THIN, (hipStream_t)s);
   return e;
 }
