@@ -18,6 +18,7 @@ prof() {  # name, timeout, args...
   timeout -k 10 "$t" rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof_$name" -o run -- python bench.py --no-cpu "$@" \
     > "$OUT/prof_$name.log" 2>&1 || { echo "prof $name failed rc=$?"; return 1; }
   find "$OUT/prof_$name" -name "*kernel_stats.csv" -exec cp {} "$OUT/${name}_kernel_stats.csv" \;
+  find "$OUT/prof_$name" -name "*kernel_trace.csv" -exec cp {} "$OUT/${name}_kernel_trace.csv" \;
   echo "prof $name ok"
 }
 if [ "$WHAT" = b ] || [ "$WHAT" = all ]; then

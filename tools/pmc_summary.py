@@ -26,7 +26,7 @@ def short(name):
     """Kernel symbol -> the C-ABI call bench.py times (kernel table names)."""
     table = [("rgb_fwd_kernel", "mli_rgb_fwd"), ("rgb_bwd_kernel", "mli_rgb_bwd"),
              ("dw4_partial_kernel", "mli_dw4"), ("dw4_reduce_kernel", "mli_dw4:reduce"),
-             ("wgrad_kernel<256, 256", "mli_wgrad:big"), ("wgrad_kernel<256, 320", "mli_wgrad:wide"),
+             ("wgrad_kernel<256, 256", "mli_wgrad:big"), ("wgrad_dma_kernel<256, 256", "mli_wgrad:big"), ("wgrad_kernel<256, 320", "mli_wgrad:wide"),
              ("wgrad_kernel<32, 256", "mli_wgrad:thin"), ("wgrad_dma_kernel<256, 320", "mli_wgrad:wide"), ("encode5_kernel", "mli_sdf:field/encode5"),
              ("field_mlp_kernel", "mli_sdf:field/mlp"), ("sdf_kernel", "mli_sdf:sdf"), ("sample_fine_kernel", "mli_sample_fine"),
              ("composite_fwd_kernel", "mli_composite_fwd"), ("composite_bwd_kernel", "mli_composite_bwd"),

@@ -3,7 +3,8 @@ which stream, when, and what overlaps.  Usage: python tools/timeline.py <run_ker
 import csv
 import sys
 
-SHORT = [("rgb_fwd", "fwd"), ("rgb_bwd", "bwd"), ("wgrad_kernel<256, 256", "BIG"), ("wgrad_dma", "WIDE"),
+SHORT = [("rgb_fwd", "fwd"), ("rgb_bwd", "bwd"), ("wgrad_kernel<256, 256", "BIG"), ("wgrad_dma_kernel<256, 256", "BIG"),
+         ("wgrad_dma", "WIDE"),
          ("wgrad_kernel<32", "THIN"), ("encode5", "enc5"), ("field_mlp", "fmlp"), ("sdf_kernel", "sdf"),
          ("sample_fine", "fine"), ("sample_coarse", "coarse"), ("composite_loss_kernel", "cl"),
          ("composite_loss_finalize", "clfin"), ("composite_fwd", "cfwd"), ("dw4_partial", "dw4p"),
