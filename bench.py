@@ -78,7 +78,7 @@ def kernel_flops(name, R, N, Nc, Nf, H, stage="b"):
     return 0
 
 
-PMC_SUMMARY = os.path.join(HERE, "profiles", "r3", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(HERE, "profiles", "r3", "m2", "pmc_summary.json")
 PMC_SAMPLES = 4096 * 128  # the workload the committed PMC passes ran (tools/pmc.sh: bench.py defaults)
 
 
@@ -464,6 +464,9 @@ def main(argv=None):
     ap.add_argument("--priority", choices=("none", "main", "side"), default="none",
                     help="pipeline: run the step on a high-priority stream (main) or give the prefetch "
                          "stream the high priority (side)")
+    ap.add_argument("--prefetch-depth", type=int, default=1, choices=(1, 2),
+                    help="pipeline: batches prefetched ahead of the trained one (2: the geometry of step "
+                         "k+2 runs beside step k and never holds up step k+1)")
     ap.add_argument("--side-cus", default=None,
                     help="pipeline experiment: restrict the prefetch stream to a CU subset "
                          "(hipExtStreamCreateWithCUMask): every:K = CUs i %% K == 0, first:K, skip:K = the complement of every:K")
@@ -574,21 +577,24 @@ def main(argv=None):
         torch.cuda.synchronize()
         torch.cuda.set_stream(main_stream)
     pipe = args.pipeline != "off" and model.stage == "b"
-    cur = next_batch()
+    depth = args.prefetch_depth if pipe else 1
+    trainer.prefetch_depth = depth
+    ahead = [next_batch() for _ in range(depth)]   # drawn (and prefetched) ahead of training
     if pipe:
-        trainer.prefetch(cur)
+        for b in ahead:
+            trainer.prefetch(b)
 
     trainer.prefetch_gate = args.pipeline if pipe else "call"
 
     def step():
-        nonlocal cur
         nxt = next_batch()
+        cur = ahead.pop(0)
+        ahead.append(nxt)
         if pipe and args.pipeline == "call":
             trainer.prefetch(nxt)
         trainer.train_step(cur)
         if pipe and args.pipeline != "call":
             trainer.prefetch(nxt)
-        cur = nxt
 
     for _ in range(args.warmup):
         step()
@@ -620,7 +626,8 @@ def main(argv=None):
     if pipe and not args.no_kernel_timing:
         # with the prefetch on, an event pair on one stream also times the other stream's
         # kernels: the per-kernel table comes from extra (untimed) steps with the pipeline off
-        trainer.train_step(cur)          # retire the prefetched batch
+        for b in ahead:                  # retire the prefetched batches
+            trainer.train_step(b)
         k_steps = 200  # >= 1 s of GPU work whatever --steps is (per-kernel averages; a busy GPU for samplers)
         L.PROFILE, L.PROFILE_NAMES = [], names
         for _ in range(k_steps):

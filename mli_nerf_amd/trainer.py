@@ -272,6 +272,10 @@ class Trainer:
         # the last two, prefetch is called after train_step
         self.prefetch_gate = "call"
         self.side_priority = 0  # torch stream priority of the prefetch stream (lower = higher)
+        # batches prefetched ahead of the one being trained (each in its own buffer lane): with 2
+        # the geometry of batch k+2 runs beside step k and may run on into step k+1 without
+        # holding it up (step k+1 trains on batch k+1, prefetched a step earlier)
+        self.prefetch_depth = 1
         self._gate_ev = None
         self.sched = o.sched
         self.current_iteration = 0
@@ -381,15 +385,17 @@ class Trainer:
         with the same dict then runs the heads onward on the prefetched geometry; its results
         equal the unpipelined step's on the same ``u`` (tests/test_gpu_parity.py).
 
-        Call order: draw the batch, ``prefetch`` it, then ``train_step`` the previous batch.
-        The side stream waits for an event recorded here on the current stream, i.e. after
-        every step issued so far, so lane L is rewritten only once the step that read it two
-        prefetches ago has been issued ahead of it.  A no-op outside the fused stage-b path."""
+        Call order: draw the batch, ``prefetch`` it, then ``train_step`` the batch
+        ``prefetch_depth`` draws earlier (with the gates ``heads`` / ``wgrad``: train, then
+        prefetch).  The side stream waits for an event recorded on the current stream (the
+        gate), i.e. after the step that last read the lane it rewrites: ``prefetch_depth + 1``
+        lanes rotate, so that step is at least the one issued before the gate's.  A no-op
+        outside the fused stage-b path."""
         m = self.model
         if self.stage != "b" or not set(self.weights) <= FUSED_LOSSES:
             return
-        if len(self._pending) >= 2:
-            raise RuntimeError("prefetch: two batches already prefetched and not yet trained on")
+        if len(self._pending) > self.prefetch_depth:
+            raise RuntimeError("prefetch: %d batches already prefetched and not yet trained on" % len(self._pending))
         m.train()
         if m.engine is None:
             m.prepare()
@@ -406,7 +412,7 @@ class Trainer:
         side = self._side
         side.wait_event(ready)
         lane = ("pf", self._pf_lane)
-        self._pf_lane ^= 1
+        self._pf_lane = (self._pf_lane + 1) % (self.prefetch_depth + 1)
         prev = eng._bufs
         try:
             with torch.cuda.stream(side):

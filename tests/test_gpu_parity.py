@@ -330,13 +330,14 @@ def test_fused_loss_step_matches_autograd_step(case):
     assert rel < 1e-5
 
 
-@pytest.mark.parametrize("gate", ["call", "heads", "wgrad"])
-def test_prefetch_pipeline_matches_serial_steps(gate):
+@pytest.mark.parametrize("gate,depth", [("call", 1), ("heads", 1), ("wgrad", 1), ("heads", 2), ("call", 2)])
+def test_prefetch_pipeline_matches_serial_steps(gate, depth):
     """Trainer.prefetch (the next batch's rays / sampling / FIELD on a side stream, into a spare
-    buffer lane, overlapping the current step's heads and backward) against plain serial
-    train_step calls: same batches and uniforms, four steps, the AdamW updates in between.
-    Loss values and parameters after every step agree to 1e-6 relative (the kernels are the
-    same; only the stream a launch is issued on and the buffer lane change)."""
+    buffer lane, overlapping the current step's heads and backward; depth 2: two batches ahead,
+    three lanes) against plain serial train_step calls: same batches and uniforms, four steps,
+    the AdamW updates in between.  Loss values and parameters after every step agree to 1e-6
+    relative (the kernels are the same; only the stream a launch is issued on and the buffer
+    lane change)."""
     _need_gpu()
     from mli_nerf_amd.trainer import Trainer
     R, Nc = 256, 16
@@ -346,24 +347,26 @@ def test_prefetch_pipeline_matches_serial_steps(gate):
         model, sd, _, _, (Hh, W) = build("syn_hotdog_b", R, Nc, 4, 4, 14, 3.0)
         tr = Trainer(cfg, is_inference=False, model=model)
         tr.prefetch_gate = gate
+        tr.prefetch_depth = depth
         g = torch.Generator().manual_seed(7)
-        batches = [to_dev(synthetic.make_batch(R, H=Hh, W=W, frame=f)) for f in range(3, 8)]
+        batches = [to_dev(synthetic.make_batch(R, H=Hh, W=W, frame=f)) for f in range(3, 9)]
         us = [torch.rand(1, R, Nc, generator=g).to(DEV) for _ in batches]
         hist = []
         if pipelined:
-            tr.prefetch(batches[0], u=us[0])
+            for j in range(depth):
+                tr.prefetch(batches[j], u=us[j])
         for k in range(4):
-            if pipelined and gate == "call":   # draw, prefetch, then train the previous batch
-                tr.prefetch(batches[k + 1], u=us[k + 1])
+            if pipelined and gate == "call":   # draw, prefetch, then train the batch drawn depth earlier
+                tr.prefetch(batches[k + depth], u=us[k + depth])
                 tr.train_step(batches[k])
             elif pipelined:                     # gated: train, then prefetch behind its gate
                 tr.train_step(batches[k])
-                tr.prefetch(batches[k + 1], u=us[k + 1])
+                tr.prefetch(batches[k + depth], u=us[k + depth])
             else:
                 tr.train_step(batches[k], u=us[k])
             hist.append((float(tr.losses["total"]), model.flat.detach().clone()))
         torch.cuda.synchronize()
-        assert not pipelined or len(tr._pending) == 1
+        assert not pipelined or len(tr._pending) == depth
         runs.append(hist)
     for k, ((l0, p0), (l1, p1)) in enumerate(zip(*runs)):
         print("step", k, "loss", l0, l1, "param max diff", (p0 - p1).abs().max().item())
