@@ -464,7 +464,7 @@ def main(argv=None):
     ap.add_argument("--priority", choices=("none", "main", "side"), default="none",
                     help="pipeline: run the step on a high-priority stream (main) or give the prefetch "
                          "stream the high priority (side)")
-    ap.add_argument("--prefetch-depth", type=int, default=1, choices=(1, 2),
+    ap.add_argument("--prefetch-depth", type=int, default=2, choices=(1, 2),
                     help="pipeline: batches prefetched ahead of the trained one (2: the geometry of step "
                          "k+2 runs beside step k and never holds up step k+1)")
     ap.add_argument("--side-cus", default=None,
@@ -650,7 +650,7 @@ def main(argv=None):
                  "synthetic (seeded cameras/lights/labels, random-init weights, full 2^22 hash table)"),
         "config": {"workload": "%s stage-%s train step" % (args.config, model.stage), "rays_per_gpu": R,
                    "samples_per_ray": N, "global_rays": R * world, "image": [Hh, W], "parallelism": "dp%d" % world,
-                   "pipeline": ("geometry prefetch on a side stream, gate " + args.pipeline) if pipe else "off",
+                   "pipeline": ("geometry prefetch on a side stream, gate %s, %d batch(es) ahead" % (args.pipeline, depth)) if pipe else "off",
                    "output_layer_dw": "forward partials (pq)" if args.pq == "on" else "THIN split-K",
                    "tail": args.tail},
         "kernel_timing": ("HIP events on the launch stream over %d extra steps with the prefetch off" % k_steps)
