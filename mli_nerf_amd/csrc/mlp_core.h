@@ -66,6 +66,10 @@ struct Geo {
   // per-wave transpose scratch of the output-layer partials (rgb_fwd PQ mode, q4_tile)
   static constexpr int PQ_WAVE = 2048 + 256;
   static constexpr int LDS_FWD_PQ = LDS_FWD + NW * PQ_WAVE;
+  // PQ mode: the first FEAT_KS k-steps of each wave's feat fragments also stay in a wave-private
+  // LDS block, so the three heads re-read only the rest from the frag image
+  static constexpr int FEAT_KS = 6;
+  static constexpr int LDS_FWD_PQF = LDS_FWD_PQ + NW * FEAT_KS * 1024;
   static constexpr int TPR = SAMPLES / 8;  // 16 B flush pieces per staged row
   // ring DMAs per wave and chunk, flush stores per wave and staged tile
   template <int ROLE> static constexpr int ring_ops() { return ROLE == STORE ? 0 : RND; }
@@ -475,6 +479,11 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
     half8* dst = reinterpret_cast<half8*>(ftile) + (2 * t) * 64 + lane;
     dst[0] = A[2 * t];
     dst[64] = A[2 * t + 1];
+    if (PQ && 2 * t + 1 < G::FEAT_KS) {  // (the image keeps every k-step: the vmcnt counts are static)
+      half8* fl = reinterpret_cast<half8*>(lds + G::LDS_FWD_PQ + wave * G::FEAT_KS * 1024) + (2 * t) * 64 + lane;
+      fl[0] = A[2 * t];
+      fl[64] = A[2 * t + 1];
+    }
     if (TRAIN) stage_tile<G>(sg, lds, A[2 * t], A[2 * t + 1], a.x0T + (size_t)(32 * t) * S + col0, lane);
   });
 
@@ -484,8 +493,9 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
     // opaque per head so the 16 addresses are not hoisted out of the head loop (spills)
     {
       const half8* src = reinterpret_cast<const half8*>(ftile) + opaque_v(lane);
+      const half8* fl = reinterpret_cast<const half8*>(lds + G::LDS_FWD_PQ + wave * G::FEAT_KS * 1024) + lane;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) B[q] = src[q * 64];
+      for (int q = 0; q < 16; ++q) B[q] = (PQ && q < G::FEAT_KS) ? fl[q * 64] : src[q * 64];
     }
     uint32_t mbits[4];
     // stg: the layer's activations go to xT (PQ: not X3, the output layer's input)
