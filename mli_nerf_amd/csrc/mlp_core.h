@@ -70,6 +70,9 @@ struct Geo {
   // LDS block, so the three heads re-read only the rest from the frag image
   static constexpr int FEAT_KS = 6;
   static constexpr int LDS_FWD_PQF = LDS_FWD_PQ + NW * FEAT_KS * 1024;
+  // the eval forward (no PQ blocks): 8 k-steps fit
+  static constexpr int FEAT_KS_EVAL = 8;
+  static constexpr int LDS_FWD_F = LDS_FWD + NW * FEAT_KS_EVAL * 1024;
   static constexpr int TPR = SAMPLES / 8;  // 16 B flush pieces per staged row
   // ring DMAs per wave and chunk, flush stores per wave and staged tile
   template <int ROLE> static constexpr int ring_ops() { return ROLE == STORE ? 0 : RND; }
@@ -407,6 +410,13 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
   const size_t slot = (size_t)k * a.R + r;
   auto bytes = [](int cc) MLI_LAMBDA_FI { return fwd_bytes(cc); };
   constexpr int XL = PQ ? 3 : 4;  // activation layers stored per head (PQ: X3 is not)
+  // feat k-steps the heads re-read from a wave-private LDS block (the rest: the frag image)
+#ifdef MLI_EVAL_FEAT_LDS
+  constexpr int FKS = PQ ? G::FEAT_KS : (!TRAIN ? G::FEAT_KS_EVAL : 0);
+#else
+  constexpr int FKS = PQ ? G::FEAT_KS : 0;
+#endif
+  constexpr int FOFF = PQ ? G::LDS_FWD_PQ : G::LDS_FWD;
   const float wgt = PQ ? a.weights[slot] : 0.f;  // composite weight of the sample (PQ)
 
   Ring rg;
@@ -479,8 +489,8 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
     half8* dst = reinterpret_cast<half8*>(ftile) + (2 * t) * 64 + lane;
     dst[0] = A[2 * t];
     dst[64] = A[2 * t + 1];
-    if (PQ && 2 * t + 1 < G::FEAT_KS) {  // (the image keeps every k-step: the vmcnt counts are static)
-      half8* fl = reinterpret_cast<half8*>(lds + G::LDS_FWD_PQ + wave * G::FEAT_KS * 1024) + (2 * t) * 64 + lane;
+    if (2 * t + 1 < FKS) {  // (the image keeps every k-step: the vmcnt counts are static)
+      half8* fl = reinterpret_cast<half8*>(lds + FOFF + wave * FKS * 1024) + (2 * t) * 64 + lane;
       fl[0] = A[2 * t];
       fl[64] = A[2 * t + 1];
     }
@@ -493,9 +503,9 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
     // opaque per head so the 16 addresses are not hoisted out of the head loop (spills)
     {
       const half8* src = reinterpret_cast<const half8*>(ftile) + opaque_v(lane);
-      const half8* fl = reinterpret_cast<const half8*>(lds + G::LDS_FWD_PQ + wave * G::FEAT_KS * 1024) + lane;
+      const half8* fl = reinterpret_cast<const half8*>(lds + FOFF + wave * (FKS > 0 ? FKS : 1) * 1024) + lane;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) B[q] = (PQ && q < G::FEAT_KS) ? fl[q * 64] : src[q * 64];
+      for (int q = 0; q < 16; ++q) B[q] = q < FKS ? fl[q * 64] : src[q * 64];
     }
     uint32_t mbits[4];
     // stg: the layer's activations go to xT (PQ: not X3, the output layer's input)
