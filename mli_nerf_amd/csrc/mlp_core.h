@@ -411,11 +411,7 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
   auto bytes = [](int cc) MLI_LAMBDA_FI { return fwd_bytes(cc); };
   constexpr int XL = PQ ? 3 : 4;  // activation layers stored per head (PQ: X3 is not)
   // feat k-steps the heads re-read from a wave-private LDS block (the rest: the frag image)
-#ifdef MLI_EVAL_FEAT_LDS
   constexpr int FKS = PQ ? G::FEAT_KS : (!TRAIN ? G::FEAT_KS_EVAL : 0);
-#else
-  constexpr int FKS = PQ ? G::FEAT_KS : 0;
-#endif
   constexpr int FOFF = PQ ? G::LDS_FWD_PQ : G::LDS_FWD;
   const float wgt = PQ ? a.weights[slot] : 0.f;  // composite weight of the sample (PQ)
 

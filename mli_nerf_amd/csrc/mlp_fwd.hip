@@ -14,11 +14,8 @@ extern "C" int mli_rgb_fwd(const mli_rgb_fwd_args* a, mli_stream_t s) {
   const dim3 grid(S / GFwd::SAMPLES), block(GFwd::THREADS);
   if (pq) return mli_launch_rgb_fwd_pq(a, (hipStream_t)s);
   if (train) return mli_launch_rgb_fwd_train(a, (hipStream_t)s);
-#ifdef MLI_EVAL_FEAT_LDS
+  static_assert(GFwd::LDS_FWD_F <= 163840, "LDS per workgroup");
   hipLaunchKernelGGL((rgb_fwd_kernel<false, false>), grid, block, GFwd::LDS_FWD_F, (hipStream_t)s, *a);
-#else
-  hipLaunchKernelGGL((rgb_fwd_kernel<false, false>), grid, block, GFwd::LDS_FWD, (hipStream_t)s, *a);
-#endif
   MLI_LAUNCH_CHECK();
 }
 

@@ -526,7 +526,7 @@ int launch(const mli_wgrad_args* a, int cls, hipStream_t s) {
                          DMA_NBUF * (BM + BN) * DMA_BKD * 2, s, ka);
     else if constexpr (SHARE_B)
       hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, DEPTH, true>), dim3(grid), dim3(512), (BM + BN) * ROWB, s, ka);
-  } else if constexpr (DMA_NBUF > 0 && !SHARE_B) {
+  } else if constexpr (DMA_NBUF > 0) {  // (a WIDE class of one job -- stage a -- shares nothing)
     hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, DMA_NBUF, false, DMA_BKD>), dim3(grid), dim3(512),
                        DMA_NBUF * (BM + BN) * DMA_BKD * 2, s, ka);
   } else {
