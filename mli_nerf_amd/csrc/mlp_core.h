@@ -559,12 +559,11 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
 // beside the other's epilogue): training forward 1.37 vs 1.29 ms, eval 0.88 vs 0.80 ms, rgb_bwd
 // 0.86 vs 0.81 ms -- the weight chunks stream through LDS once per workgroup, so halving the
 // workgroup doubles the ring DMA and LDS-write work per sample.
-#ifndef MLI_HEADS_PF
-#define MLI_HEADS_PF 4
-#endif
-typedef Geo<8, 20, true> GFwd;                 // eval forward
-typedef Geo<8, 20, true, MLI_HEADS_PF> GFwdT;  // training forward (same layout, PF 4)
-typedef Geo<8, 17, true, MLI_HEADS_PF> GBwd;
+// weight-fragment read depth of the training kernels (PF 3 / 4 / 6 measured: profiles/r3/heads_pf)
+constexpr int HEADS_PF = 4;
+typedef Geo<8, 20, true> GFwd;             // eval forward
+typedef Geo<8, 20, true, HEADS_PF> GFwdT;  // training forward (same layout)
+typedef Geo<8, 17, true, HEADS_PF> GBwd;
 
 // the first / second half of the waves take the DMA / STORE roles (see Role), compiled as two
 // programs
