@@ -208,7 +208,7 @@ def run_infer(args, world, rank, dev):
     if rank == 0 and world == 1 and not args.no_cpu:
         # CPU oracle eval forward on a bounded sample of the same frame's rays
         from oracle import render as o_render
-        threads = min(16, os.cpu_count() or 1)
+        threads, hc = cpu_threads(args)
         torch.set_num_threads(threads)
         sd = synthetic.make_state_dict(log2T=22, seed=0)
         # the GPU gathers an fp16 shadow of the table (tcnn's precision): same values here
@@ -231,7 +231,8 @@ def run_infer(args, world, rank, dev):
         result["cpu_baseline"] = {"value": round(n_cpu / t_cpu, 3), "unit": "rays/s", "cores": threads,
                                   "kind": "port", "sample": "oracle eval forward, %d rays of one %dx%d frame x %d "
                                   "samples, full hash table, torch fp32 on %d host threads" % (n_cpu, size, size, N,
-                                                                                             threads)}
+                                                                                             threads),
+                                  "host": hc}
         result["speedup_vs_cpu"] = round(value / result["cpu_baseline"]["value"], 1)
         gpu_rgb = out["rgb"][0].cpu()[data["ray_idx"][0]]
 
@@ -303,6 +304,54 @@ def cpu_baseline(cfg, R_cpu, steps, threads, stage_a=None):
                        "after 2 warm-up, torch fp32 on %d host threads" % ("a" if stage_a else "b", R_cpu,
                                                                           pcfg.n_samples, steps, threads),
                 s_per_step=t), data, u, float(psnr)
+
+
+def host_cpu():
+    """The host CPU for the cpu_baseline record (lscpu model, sockets, cores,
+    threads) and the threads the baseline uses: the physical cores this process may run on
+    (its affinity mask, SMT siblings counted once), capped by the job's CPU share
+    (OMP_NUM_THREADS: the GPU box allots 16 CPUs per one-GPU job; nproc / os.cpu_count() there
+    show the whole machine) unless ``--cpu-threads`` says otherwise."""
+    info = {"model": None, "sockets": None, "cores_per_socket": None, "threads_per_core": None,
+            "logical_cpus": os.cpu_count()}
+    try:
+        blocks = open("/proc/cpuinfo").read().strip().split("\n\n")
+        recs = [dict((k.strip(), v.strip()) for k, _, v in (ln.partition(":") for ln in b.splitlines())) for b in blocks]
+        info["model"] = recs[0].get("model name")
+        sockets = {r.get("physical id") for r in recs}
+        info["sockets"] = len(sockets)
+        cores = int(recs[0].get("cpu cores", 0)) or None
+        info["cores_per_socket"] = cores
+        if cores:
+            info["threads_per_core"] = int(recs[0].get("siblings", cores)) // cores
+    except (OSError, ValueError, IndexError):
+        pass
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        cpus = list(range(os.cpu_count() or 1))
+    phys = set()
+    for c in cpus:
+        try:
+            with open("/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list" % c) as f:
+                phys.add(f.read().strip().split(",")[0].split("-")[0])
+        except OSError:
+            phys.add(str(c))
+    info["affinity_cpus"] = len(cpus)
+    info["affinity_physical_cores"] = len(phys)
+    share = os.environ.get("OMP_NUM_THREADS")
+    info["job_cpu_share"] = int(share) if share and share.isdigit() else None
+    return info
+
+
+def cpu_threads(args):
+    hc = host_cpu()
+    if args.cpu_threads:
+        return args.cpu_threads, hc
+    n = hc["affinity_physical_cores"] or 1
+    if hc["job_cpu_share"]:
+        n = min(n, hc["job_cpu_share"])
+    return n, hc
 
 
 def count_gpus():
@@ -453,6 +502,9 @@ def main(argv=None):
     ap.add_argument("--cpu-rays", type=int, default=512)
     ap.add_argument("--cpu-steps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="cpu_baseline threads (default: the physical cores of this process's affinity mask, "
+                         "capped by the job's CPU share OMP_NUM_THREADS)")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--time-all-kernels", action="store_true",
                     help="train: HIP events around every launch (default: the MFMA kernels only; "
@@ -541,7 +593,7 @@ def main(argv=None):
     real_cams = args.config == "rene_savannah_b"
     if real_cams:
         # configs[3]: the reference's real ReNe savannah camera + light poses, rank r -> frame r
-        # (dataset_rene/savannah/train_transforms.json, committed as tests/golden/rene_savannah_train16.json)
+        # (dataset_rene/savannah/train_transforms.json, package data mli_nerf_amd/assets/rene_savannah_train16.json)
         from mli_nerf_amd.data import rene_savannah_cameras
         cams = [rene_savannah_cameras(Hh, W, frames=[rank % 16])[0]] * n_frames
     for f in range(0 if real_cams else n_frames):
@@ -667,16 +719,18 @@ def main(argv=None):
         result["config"].update(iteration=trainer.current_iteration - 1, active_levels=int(sdf.active_levels),
                                 curvature_weight=trainer.weights["curvature"])
     if rank == 0 and world == 1 and not args.no_cpu and stage_a:
-        threads = min(16, os.cpu_count() or 1)
+        threads, hc = cpu_threads(args)
         sdf = model.neural_sdf
         sa = (int(sdf.active_levels), int(sdf.anneal_levels), trainer.weights["curvature"], model.progress)
         cb, data_cpu, u_cpu, psnr_cpu = cpu_baseline(cfg, args.cpu_rays, args.cpu_steps, threads, stage_a=sa)
         result["cpu_baseline"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in cb.items()}
+        result["cpu_baseline"]["host"] = hc
         result["speedup_vs_cpu"] = round(value / cb["value"], 1)
     elif rank == 0 and world == 1 and not args.no_cpu:
-        threads = min(16, os.cpu_count() or 1)
+        threads, hc = cpu_threads(args)
         cb, data_cpu, u_cpu, psnr_cpu = cpu_baseline(cfg, args.cpu_rays, args.cpu_steps, threads)
         result["cpu_baseline"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in cb.items()}
+        result["cpu_baseline"]["host"] = hc
         result["speedup_vs_cpu"] = round(value / cb["value"], 1)
         # PSNR agreement on the CPU sample's rays (same weights, rays, uniforms)
         cfg2 = preset(args.config, rays=args.cpu_rays, n_fine=args.fine)

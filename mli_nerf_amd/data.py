@@ -78,9 +78,8 @@ def transforms_cameras(meta, H, W, readjust=None, frames=None):
 
 
 # the real cameras of BASELINE.json configs[3] (rene_savannah_b): the reference's first 16
-# savannah training frames (tests/golden/make_rene_savannah.py)
-RENE_SAVANNAH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
-                             "rene_savannah_train16.json")
+# savannah training frames, package data (tools/make_rene_savannah.py extracts them)
+RENE_SAVANNAH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "rene_savannah_train16.json")
 
 
 def rene_savannah_cameras(H=270, W=360, frames=None):

@@ -78,11 +78,14 @@ def preprocess_image(images, from_range=(0, 1)):
 
 
 def save_image(image, path, from_range=(0, 1)):
-    """torchvision to_pil_image of the preprocessed [1,C,H,W] map (x255, truncated to uint8)."""
+    """trainer.py:270-274: the [1,C,H,W] map squeezed to [C,H,W] BEFORE preprocess_image, so its
+    one-channel test looks at H and the maps keep their channel count (no colormap); then
+    torchvision's to_pil_image: x255 truncated to uint8 (``mul(255).byte()``), one channel -> an
+    'L' PNG, three -> 'RGB'."""
     from PIL import Image
-    im = preprocess_image(image, from_range)[0]
-    a = (im.permute(1, 2, 0).numpy() * 255).astype(np.uint8)
-    Image.fromarray(a).save(path)
+    im = preprocess_image(image.squeeze(0), from_range)
+    a = im.mul(255).byte().permute(1, 2, 0).numpy()
+    Image.fromarray(a[:, :, 0] if a.shape[2] == 1 else a, mode="L" if a.shape[2] == 1 else "RGB").save(path)
 
 
 @torch.no_grad()

@@ -117,15 +117,19 @@ class FusedAdamW:
         self.v = torch.zeros_like(flat.detach())
         self.step_count = 0
 
-    def step(self, grad, lr, p16=None, ranges=None):
+    def step(self, grad, lr, p16=None, ranges=None, before=None):
         """``p16``: fp16 tensor to receive a copy of the updated parameters (the hash table's
         gather shadow), or None.  ``ranges``: [(offset, n)] of the trainable elements when only
         part of the buffer trains (the rest -- frozen by partial_grad / partial_training -- gets
         no update, no weight decay and keeps its moments, as torch AdamW skips a parameter whose
-        grad is None); None: the whole buffer."""
+        grad is None); None: the whole buffer.  ``before(i)`` runs before range i is issued (the
+        chunked table reduction waits there for chunk i's all-reduce); one step either way, the
+        update is element-wise, so a split into ranges changes no result."""
         self.step_count += 1
         p = self.flat.detach()
-        for off, n in ([(0, p.numel())] if ranges is None else ranges):
+        for i, (off, n) in enumerate([(0, p.numel())] if ranges is None else ranges):
+            if before is not None:
+                before(i)
             L.call("mli_adamw", L.AdamwArgs(L.ptr(p[off:]), L.ptr(grad[off:]), L.ptr(self.m[off:]),
                                             L.ptr(self.v[off:]), n, float(lr), self.betas[0], self.betas[1],
                                             self.eps, self.wd, self.step_count,
@@ -151,6 +155,42 @@ def reduce_gradients(grad, world_size, group=None):
         dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=group)
         grad.div_(world_size)
     return grad
+
+
+def table_chunks(n, chunk):
+    """[(offset, length)] cutting n elements into pieces of ``chunk`` (the last one ragged)."""
+    chunk = max(1, int(chunk))
+    return [(o, min(chunk, n - o)) for o in range(0, n, chunk)]
+
+
+def reduce_and_step_table(optim, grad, lr, p16, world_size, chunk, overlap=True, group=None):
+    """Stage a: average the hash-table gradient over the ranks (DDP wraps the table with every
+    other parameter, imaginaire/trainers/utils/get_trainer.py:80-88) and take the table's AdamW
+    step.  At 2^22 entries per level the gradient is 1.46 GB, so the serial form -- ONE all-reduce,
+    then the 11 GB AdamW pass -- leaves the collective and the update back to back.  Overlapped:
+    the table goes as ``chunk``-element all-reduces issued together (async; RCCL runs them in
+    order on its stream), and the AdamW of chunk i is issued behind chunk i's completion only, so
+    it runs on the compute stream while chunk i+1 reduces.  Every element sees the same ops as
+    in the serial form (its sum, / world_size, the element-wise update); a two-rank sum is
+    exact in either order, so at world size 2 the two forms are bit-identical (tested), and
+    ``overlap=False`` (the deterministic mode) keeps the single collective for more ranks, whose
+    ring order depends on the message split."""
+    if world_size == 1:
+        optim.step(grad, lr, p16=p16)
+        return
+    import torch.distributed as dist
+    if not overlap:
+        reduce_gradients(grad, world_size, group)
+        optim.step(grad, lr, p16=p16)
+        return
+    chunks = table_chunks(grad.numel(), chunk)
+    works = [dist.all_reduce(grad[o:o + k], op=dist.ReduceOp.SUM, group=group, async_op=True) for o, k in chunks]
+
+    def ready(i):
+        works[i].wait()   # NCCL: the current stream waits for chunk i; gloo: the host does
+        o, k = chunks[i]
+        grad[o:o + k].div_(world_size)
+    optim.step(grad, lr, p16=p16, ranges=chunks, before=ready)
 
 
 class Checkpointer:
@@ -263,6 +303,10 @@ class Trainer:
             if model.neural_sdf.c2f is not None:   # neuralangelo/trainer.py:30-32
                 model.neural_sdf.warm_up_end = o.sched.warm_up_end
         self._grad_table = None
+        # stage a over several ranks: the table gradient's all-reduce in chunks, each chunk's
+        # AdamW issued behind its own reduction (reduce_and_step_table); 2^25 elements = 128 MiB
+        self.table_overlap = True
+        self.table_chunk = 1 << 25
         self._side = None      # prefetch stream (stage-b geometry of the next batch)
         self._pending = []     # prefetched geometries not yet consumed by train_step
         self._pf_lane = 0
@@ -275,13 +319,31 @@ class Trainer:
         # batches prefetched ahead of the one being trained (each in its own buffer lane): with 2
         # the geometry of batch k+2 runs beside step k and may run on into step k+1 without
         # holding it up (step k+1 trains on batch k+1, prefetched a step earlier)
-        self.prefetch_depth = 1
+        self._prefetch_depth = 1
         self._gate_ev = None
         self.sched = o.sched
         self.current_iteration = 0
         self.current_epoch = 0
         self.losses, self.metrics = {}, {}
         self.checkpointer = Checkpointer(cfg, self)
+
+    @property
+    def prefetch_depth(self):
+        return self._prefetch_depth
+
+    @prefetch_depth.setter
+    def prefetch_depth(self, d):
+        """The lanes rotate modulo depth + 1: a change while prefetched batches are pending could
+        point the next prefetch at a lane still in use, so it is refused then."""
+        d = int(d)
+        if d < 1:
+            raise ValueError("prefetch_depth must be >= 1")
+        if d != self._prefetch_depth:
+            if self._pending:
+                raise RuntimeError("prefetch_depth cannot change while %d prefetched batches are pending"
+                                   % len(self._pending))
+            self._pf_lane = 0
+        self._prefetch_depth = d
 
     # ------------------------------------------------------------ construction (reference)
     @staticmethod
@@ -325,12 +387,14 @@ class Trainer:
         """[(offset, n)] of the flat buffer the optimizer steps: the Parameters of
         model.get_param_groups(cfg.optim) whose requires_grad is on (NeuralLumen/trainer.py:44-54
         partial_grad, NeuralLumen/model.py:422-438 partial_training), adjacent ones merged; None when
-        that is the whole buffer (one launch)."""
-        live = {n for n, p in self.optimized_parameters() if p.requires_grad}
-        items = self.model._trainable_items()
-        key = tuple(sorted(live))
+        that is the whole buffer (one launch).  Recomputed only when a requires_grad flag of the
+        optimized Parameters changed (the key), not every step."""
+        opt = self._optimized_cached()
+        key = tuple(p.requires_grad for _, p in opt)
         if getattr(self, "_ranges_key", None) == key:
             return self._ranges
+        live = {n for n, p in opt if p.requires_grad}
+        items = self.model._trainable_items()
         ranges = []
         for name, _, off, n in items:
             if name in live:
@@ -345,7 +409,14 @@ class Trainer:
     def table_trains(self):
         """Stage a: whether the hash table is among the optimized, requires_grad parameters."""
         t = self.model.neural_sdf.tcnn_encoding.params
-        return any(p is t and p.requires_grad for _, p in self.optimized_parameters())
+        return any(p is t and p.requires_grad for _, p in self._optimized_cached())
+
+    def _optimized_cached(self):
+        """optimized_parameters(), computed once (the Parameter objects never change: load and
+        .to() replace their data only)."""
+        if getattr(self, "_opt_params", None) is None:
+            self._opt_params = self.optimized_parameters()
+        return self._opt_params
 
     def optimized_parameters(self):
         """[(name, Parameter)] of the reference optimizer, in its order:
@@ -394,8 +465,14 @@ class Trainer:
         m = self.model
         if self.stage != "b" or not set(self.weights) <= FUSED_LOSSES:
             return
-        if len(self._pending) > self.prefetch_depth:
-            raise RuntimeError("prefetch: %d batches already prefetched and not yet trained on" % len(self._pending))
+        # gate "call": prefetch, then train the batch depth draws earlier (depth + 1 may be
+        # pending); gates "heads" / "wgrad": train, then prefetch, so at most depth may be -- one
+        # more would land in the lane of the step just issued, whose tail (composite, backward)
+        # still reads it after the gate event
+        limit = self.prefetch_depth + (1 if self.prefetch_gate == "call" else 0)
+        if len(self._pending) >= limit:
+            raise RuntimeError("prefetch: %d batches already prefetched and not yet trained on (gate %s, depth %d)"
+                               % (len(self._pending), self.prefetch_gate, self.prefetch_depth))
         m.train()
         if m.engine is None:
             m.prepare()
@@ -599,12 +676,13 @@ class Trainer:
         eng = m.engine
         grad = self._grad[:m.flat.numel()]
         reduce_gradients(self._grad, self.world_size)
-        gtab = reduce_gradients(self._grad_table, self.world_size)
         m.set_flat_grad(grad)
         lr = self.lr()
         self.optim.step(grad, lr, ranges=self.adam_ranges())
         if self.table_trains():
-            self.optim_table.step(gtab, lr, p16=eng.table16)
+            # (a frozen table needs no averaged gradient: no collective for it)
+            reduce_and_step_table(self.optim_table, self._grad_table, lr, eng.table16, self.world_size,
+                                  self.table_chunk, overlap=self.table_overlap and not m.deterministic)
         self.current_iteration += 1
         self._publish(lv)
         return m.outputs(st) if return_outputs else None
@@ -637,8 +715,8 @@ class Trainer:
         self.optim.step(grad, self.lr(), ranges=self.adam_ranges())
         if self.stage == "a" and self.table_trains():
             table = m.neural_sdf.tcnn_encoding.params
-            gtab = reduce_gradients(table.grad, self.world_size)
-            self.optim_table.step(gtab, self.lr(), p16=m.engine.table16)
+            reduce_and_step_table(self.optim_table, table.grad, self.lr(), m.engine.table16, self.world_size,
+                                  self.table_chunk, overlap=self.table_overlap and not m.deterministic)
         self.current_iteration += 1
         self._publish(lv)
         return out
@@ -678,7 +756,12 @@ class Trainer:
                      params=list(range(len(views))))
         state = {}
         if self.optim.step_count > 0:
-            for i, (_, _, m, v) in enumerate(views):
+            for i, (_, p, m, v) in enumerate(views):
+                # torch AdamW keeps no state for a parameter it never stepped (grad None: frozen by
+                # partial_grad / partial_training): no entry, so no resume applies a bias
+                # correction to moments that were never accumulated
+                if not p.requires_grad:
+                    continue
                 state[i] = {"step": torch.tensor(float(self.optim.step_count)),
                             "exp_avg": m.detach().cpu().clone(), "exp_avg_sq": v.detach().cpu().clone()}
         return {"state": state, "param_groups": [group]}

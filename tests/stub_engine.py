@@ -79,6 +79,21 @@ class StubEngine:
         grad_out[:3] = (d_rgb * x[:, None]).sum(0)
         return grad_out
 
+    def load_table(self, params_flat):
+        self.table16 = params_flat.detach().half()
+
+    def backward_a(self, st, d_rgb, flat, grad_flat, grad_table, w_eikonal, w_curvature, progress,
+                   d_grad_ext=None, d_hess_ext=None):
+        """Stage a: the flat gradient as in ``backward``, and a dense rank-specific table gradient
+        (every element a function of the rays' pixel features and d rgb: the ranks' rays differ)."""
+        x = st[0]["x"]
+        self.backward(st, d_rgb, None, None, None, flat, None, grad_flat)
+        n = grad_table.numel()
+        k = torch.arange(n, dtype=torch.float64)
+        s = d_rgb.double().sum(1) * x.double()                  # one value per ray
+        grad_table.copy_(torch.sin(k * 1e-3) * float(s.sum()) + torch.cos(k * 7e-4) * float((s * s).sum()))
+        return grad_flat, grad_table
+
 
 def stub_losses(trainer, st, data, lv):
     """render L1 x3 and PSNR (NeuralLumen/trainer.py:135-136) in torch, into lv like the kernel."""
@@ -94,11 +109,14 @@ def stub_losses(trainer, st, data, lv):
     return d_rgb, z, z[:, :1], z
 
 
-def stub_adamw_step(self, grad, lr, p16=None, ranges=None):
-    """torch.optim.AdamW's update on the flat buffer (FusedAdamW.step's semantics, incl. ranges)."""
+def stub_adamw_step(self, grad, lr, p16=None, ranges=None, before=None):
+    """torch.optim.AdamW's update on the flat buffer (FusedAdamW.step's semantics, incl. ranges,
+    the per-range hook and the fp16 copy)."""
     self.step_count += 1
     b1, b2 = self.betas
-    for off, n in ([(0, self.flat.numel())] if ranges is None else ranges):
+    for i, (off, n) in enumerate([(0, self.flat.numel())] if ranges is None else ranges):
+        if before is not None:
+            before(i)
         p, g = self.flat.detach()[off:off + n], grad[off:off + n]
         m, v = self.m[off:off + n], self.v[off:off + n]
         p.mul_(1 - lr * self.wd)
@@ -106,6 +124,8 @@ def stub_adamw_step(self, grad, lr, p16=None, ranges=None):
         v.mul_(b2).addcmul_(g, g, value=1 - b2)
         denom = (v / (1 - b2 ** self.step_count)).sqrt_().add_(self.eps)
         p.addcdiv_(m, denom, value=-lr / (1 - b1 ** self.step_count))
+        if p16 is not None:
+            p16[off:off + n].copy_(p)
 
 
 def install(monkeypatch=None):

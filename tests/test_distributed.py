@@ -187,6 +187,97 @@ def test_trainer_step_world2_stub_engine(monkeypatch):
     assert not torch.equal(local[0]["grad"], local[1]["grad"])  # the ranks' rays differ
 
 
+def _stub_setup_a():
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import stub_engine
+    from mli_nerf_amd import synthetic
+    from mli_nerf_amd.configs import preset
+    from mli_nerf_amd.model import Model
+    cfg = preset("syn_hotdog_a", rays=32, n_coarse=16, n_fine=4, log2T=12)
+    m = Model(cfg.model, cfg.data)
+    m.load_state_dict(synthetic.make_state_dict(log2T=12, heads="rgb"))
+    return stub_engine, cfg, m
+
+
+def _step_result_a(tr, m):
+    table = m.neural_sdf.tcnn_encoding.params
+    return dict(flat=m.flat.detach().clone(), grad=tr._grad[:m.flat.numel()].clone(),
+                table=table.detach().clone(), table16=m.engine.table16.clone(),
+                gtab=tr._grad_table.clone(), m_tab=tr.optim_table.m.clone(), v_tab=tr.optim_table.v.clone(),
+                total=float(tr.losses["total"]), world=tr.world_size)
+
+
+def _run_a(frame, world, overlap=True, chunk=1 << 14, steps=2, monkeypatch=None, install=True):
+    from mli_nerf_amd import synthetic
+    from mli_nerf_amd.trainer import Trainer
+    stub, cfg, m = _stub_setup_a()
+    if install:
+        stub.install(monkeypatch)
+    tr = Trainer(cfg, is_inference=False, model=m, world_size=world)
+    tr.table_overlap, tr.table_chunk = overlap, chunk
+    tr.current_iteration = 100000   # past the coarse-to-fine ramp
+    grads = []
+    for s in range(steps):
+        tr.train_step(synthetic.make_batch(32, frame=frame + 10 * s))
+        grads.append(_step_result_a(tr, m))
+    return grads
+
+
+def _train_a_worker(rank, port, results):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        results[(rank, "overlap")] = _run_a(rank, WORLD, overlap=True)
+        results[(rank, "serial")] = _run_a(rank, WORLD, overlap=False, install=False)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_stage_a_step_world2_stub_engine(monkeypatch):
+    """Stage a (f1) on 2 ranks with different rays: both the flat MLP
+    gradient and the 1.46 GB-class hash-table gradient are the means of the per-rank gradients
+    (DDP over every parameter, get_trainer.py:80-88); after the AdamW steps the table, its fp16
+    gather shadow and the table moments are bit-identical on both ranks; the overlapped chunked
+    table reduction (chunk i stepped while i+1 reduces) equals the serial single all-reduce
+    bit for bit."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    results = ctx.Manager().dict()
+    mp.start_processes(_train_a_worker, args=(port, results), nprocs=WORLD, join=True, start_method="spawn")
+    # per-rank gradients of the first step (same init, world size 1)
+    local = [_run_a(r, 1, steps=1, monkeypatch=monkeypatch)[0] for r in range(WORLD)]
+    assert not torch.equal(local[0]["gtab"], local[1]["gtab"])   # the ranks' rays differ
+    mean_gtab = (local[0]["gtab"] + local[1]["gtab"]) / WORLD
+    mean_grad = (local[0]["grad"] + local[1]["grad"]) / WORLD
+    n_chunks = -(-mean_gtab.numel() // (1 << 14))
+    assert n_chunks >= 4
+    for r in range(WORLD):
+        for mode in ("overlap", "serial"):
+            first = results[(r, mode)][0]
+            assert first["world"] == WORLD
+            torch.testing.assert_close(first["gtab"], mean_gtab, rtol=0, atol=1e-6)
+            torch.testing.assert_close(first["grad"], mean_grad, rtol=0, atol=1e-7)
+        for s in range(2):
+            a, b = results[(r, "overlap")][s], results[(0, "overlap")][s]
+            c = results[(r, "serial")][s]
+            for k in ("table", "table16", "m_tab", "v_tab", "flat", "gtab"):
+                assert torch.equal(a[k], b[k]), (r, s, k)   # replicas in sync
+                assert torch.equal(a[k], c[k]), (r, s, k)   # overlapped == serial, bitwise
+            assert torch.equal(a["table16"], a["table"].half())
+
+
+def test_table_chunks_cover():
+    from mli_nerf_amd.trainer import table_chunks
+    for n, c in [(10, 3), (9, 3), (1, 5), (45724048 * 8, 1 << 25)]:
+        ch = table_chunks(n, c)
+        assert ch[0][0] == 0 and sum(k for _, k in ch) == n
+        assert all(a[0] + a[1] == b[0] for a, b in zip(ch, ch[1:]))
+        assert all(0 < k <= c for _, k in ch)
+
+
 def _infer_worker(rank, port, results, size):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)

@@ -15,7 +15,11 @@ localises to one kernel.  Tolerances are stated per stage:
 * composite given identical inputs: 1e-4;
 * end to end (stage-b forward): rgb / o_r / o_s mean abs 2e-3, PSNR of the difference
   >= 40 dB, max 0.1 (a ray whose hierarchical samples move is allowed to differ);
-* weight gradients: cosine similarity >= 0.99 per tensor, relative norm error <= 5 %.
+* weight gradients: cosine similarity >= 0.999 per tensor, relative norm error <= 1 %
+  (round 3 asserted 0.99 / 5 %).
+
+Every bar goes through ``margins.check``, so a run with MLI_MARGINS_OUT set records the measured
+value beside it (profiles/r4/.../margins.json).
 """
 import math
 
@@ -26,6 +30,7 @@ import torch.nn.functional as F
 
 from mli_nerf_amd import synthetic
 from mli_nerf_amd.configs import preset
+from margins import check
 from oracle import hashgrid as o_hash, render as o_render
 
 pytestmark = pytest.mark.gpu
@@ -84,7 +89,7 @@ def test_hashgrid_encode_full_table():
     ref = o_hash.encode(x, params.float(), table)
     err = (out.cpu() - ref).abs().max().item()
     print("hashgrid max err", err)
-    assert err < 1e-5
+    check("hashgrid encode max abs", err, 1e-5, "<")
 
 
 def test_stagewise_forward():
@@ -159,11 +164,14 @@ def test_stagewise_forward():
     rgb_ref = (y[None, ..., 0:3] * w).sum(2) + (1 - w.sum(2))
     c_err = (comp["rgb"].cpu() - rgb_ref[0]).abs().max().item()
     print("composite weights err %.3g rgb err %.3g" % (w_err, c_err))
-    assert sdf_err < 2e-3
-    assert ang99 < 1.0 and ang < 10.0 and nrm_rel < 0.02
-    assert max(e_rgb, e_r, e_s) < 5e-3
-    assert w_err < 1e-4 and c_err < 1e-4
-    assert d_err < 1e-3
+    check("sdf max abs", sdf_err, 2e-3, "<")
+    check("normal angle p99 deg", ang99, 1.0, "<")
+    check("normal angle max deg", ang, 10.0, "<")
+    check("|grad| rel p99", nrm_rel, 0.02, "<")
+    check("heads max abs", max(e_rgb, e_r, e_s), 5e-3, "<")
+    check("composite weights max abs", w_err, 1e-4, "<")
+    check("composite rgb max abs", c_err, 1e-4, "<")
+    check("sampler per-round max abs", d_err, 1e-3, "<")
 
 
 def check_sampler_rounds(trace, dists_gpu, sd, pcfg, c, v, near, far, u):
@@ -210,7 +218,9 @@ def test_end_to_end_forward_backward(case):
         d = (out[key].detach().cpu() - o_free[key]).abs()
         psnr_d = -10 * math.log10(max(float((d ** 2).mean()), 1e-20))
         print("%s %s (free) max %.3g mean %.3g psnr(diff) %.1f dB" % (case, key, d.max(), d.mean(), psnr_d))
-        assert d.max() < 0.1 and d.mean() < 2e-3 and psnr_d > 40, key
+        check("%s free max abs" % key, d.max(), 0.1, "<")
+        check("%s free mean abs" % key, d.mean(), 2e-3, "<")
+        check("%s free psnr of diff dB" % key, psnr_d, 40, ">")
     # oracle conditioned on the GPU's sampled dists (sampler checked per round elsewhere):
     # forward + losses + gradients
     sd_o = {k: v.clone().requires_grad_(k.startswith("neural_rgb")) for k, v in sd16.items()}
@@ -223,11 +233,13 @@ def test_end_to_end_forward_backward(case):
         psnr_d = -10 * math.log10(max(float((d ** 2).mean()), 1e-20))
         print("%s %s max %.3g mean %.3g psnr(diff) %.1f dB" % (case, key, d.max(), d.mean(), psnr_d))
         # max abs 2e-3 on composites for a reduced-precision MFMA path (measured ~1e-4)
-        assert d.max() <= 2e-3 and d.mean() < 5e-4 and psnr_d > 50, key
-    assert abs(psnr.item() - o_psnr.item()) < 0.1, (psnr.item(), o_psnr.item())
+        check("%s max abs" % key, d.max(), 2e-3, "<=")
+        check("%s mean abs" % key, d.mean(), 5e-4, "<")
+        check("%s psnr of diff dB" % key, psnr_d, 50, ">")
+    check("train psnr delta dB", abs(psnr.item() - o_psnr.item()), 0.1, "<")
     for k in ("render", "intrinsic", "regularize_re"):
         a, b = losses[k].item(), o_losses[k].item()
-        assert abs(a - b) <= 1e-2 * max(abs(b), 1e-3) + 1e-4, (k, a, b)
+        check("loss %s rel" % k, abs(a - b) / (max(abs(b), 1e-3) + 1e-2), 1e-2, "<=")
     lay = model.engine.tlayout
     worst = 1.0
     for name, shape, off in lay:
@@ -237,7 +249,8 @@ def test_end_to_end_forward_backward(case):
         cos = F.cosine_similarity(g.flatten(), o.flatten(), dim=0).item() if o.norm() > 0 else 1.0
         rel = ((g - o).norm() / max(o.norm().item(), 1e-12)).item()
         worst = min(worst, cos)
-        assert cos > 0.99 and rel < 0.05, (name, cos, rel)
+        check("grad cos " + name, cos, 0.999, ">=")
+        check("grad rel " + name, rel, 0.01, "<=")
     print("%s grads: worst cosine %.5f" % (case, worst))
 
 
@@ -270,7 +283,9 @@ def test_inference_full_image():
         d = (out[key].cpu().reshape(ref[key].shape) - ref[key]).abs()
         psnr_d = -10 * math.log10(max(float((d ** 2).mean()), 1e-20))
         print("inference %s max %.3g mean %.3g psnr(diff) %.1f dB" % (key, d.max(), d.mean(), psnr_d))
-        assert d.max() < 0.1 and d.mean() < 2e-3 and psnr_d > 40, key
+        check("inference %s max abs" % key, d.max(), 0.1, "<")
+        check("inference %s mean abs" % key, d.mean(), 2e-3, "<")
+        check("inference %s psnr of diff dB" % key, psnr_d, 40, ">")
     # the maps are the per-ray outputs laid out [B, C, H, W]
     torch.testing.assert_close(out["rgb_map"][0].permute(1, 2, 0).reshape(-1, 3), out["rgb"][0])
 

@@ -16,6 +16,7 @@ import pytest
 import torch
 
 from mli_nerf_amd import synthetic
+from margins import check
 from mli_nerf_amd.configs import preset
 from oracle import render as o_render
 
@@ -78,16 +79,18 @@ def test_light_visibility_matches_oracle(config):
     assert hit.sum() > 20
     for k in ("inter_mask", "visibility"):
         agree = (g[k] == ref[k]).float().mean().item()
-        assert agree >= 0.97, (k, agree)
+        check(k + " agreement", agree, 0.97, ">=")
     both = (g["inter_mask"] == ref["inter_mask"]) & (g["visibility"] == ref["visibility"])
     err = (g["inter_dist"] - ref["inter_dist"]).abs()[both]
-    assert err.mean().item() <= 2e-4 and err.max().item() <= 1e-2, (err.mean().item(), err.max().item())
+    check("inter_dist mean abs", err.mean().item(), 2e-4, "<=")
+    check("inter_dist max abs", err.max().item(), 1e-2, "<=")
     # the shading terms are the 4-tap normal at the traced intersection (inter_dist above: <= 1e-2
     # apart) dotted with the light: 2e-3 (measured 0.4-1.1e-3; fp32 pre-activation rounding, fma
     # vs mul + add, moves the 1.8e3x-amplified tap differences by that much)
     for k in ("normal_x_light", "pseudo_shading"):
-        err = (g[k] - ref[k]).abs()[both].max().item()
-        assert err <= 2e-3, (k, err)
+        e = (g[k] - ref[k]).abs()[both]
+        check(k + " p99 abs", torch.quantile(e, 0.99).item(), 1e-3, "<=")
+        check(k + " max abs", e.max().item(), 2e-3, "<=")
     if config == "syn_hotdog_a":  # the case has shadowed surface hits
         assert 0.0 < g["visibility"][0, hit, 0].float().mean().item() < 1.0
 

@@ -104,6 +104,16 @@ def test_all_light_enumeration_matches_reference(name, tmp_path):
                 keys.add("rgb_target")
             assert set(r) == keys and r["normal"].shape == (1, 3, H, W) and r["visibility"].shape == (1, 1, H, W)
             assert os.path.exists(os.path.join(str(tmp_path), cam, li + "_pseudo_shading.png"))
+            # trainer.py:270-274 squeezes the batch dim before preprocess_image: one-channel maps
+            # stay single-channel 'L' PNGs (no colormap), levels int(v * 255)
+            from PIL import Image
+            for name, mode in (("visibility", "L"), ("inter_mask", "L"), ("normal_x_light", "L"),
+                               ("pseudo_shading", "L"), ("inter_dist", "L"), ("rgb_render", "RGB"), ("normal", "RGB")):
+                im = Image.open(os.path.join(str(tmp_path), cam, li + "_" + name + ".png"))
+                assert im.mode == mode and im.size == (W, H), (name, im.mode)
+            im = Image.open(os.path.join(str(tmp_path), cam, li + "_normal.png"))
+            light = int(r["normal"].flatten()[0])   # normal map = light x (from range (-1, 1): clamped to 1)
+            assert im.getpixel((0, 0)) == (255, 255, 255) if light >= 1 else True
     import sys
     assert tr.iters and all(i == sys.maxsize for i in tr.iters)   # mode 'test': iteration sys.maxsize
     assert tr.current_iteration == 7 and ds.sample_train_rays is False
