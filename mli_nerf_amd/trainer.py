@@ -304,8 +304,9 @@ class Trainer:
                 model.neural_sdf.warm_up_end = o.sched.warm_up_end
         self._grad_table = None
         # stage a over several ranks: the table gradient's all-reduce in chunks, each chunk's
-        # AdamW issued behind its own reduction (reduce_and_step_table); 2^25 elements = 128 MiB
-        self.table_overlap = True
+        # AdamW issued behind its own reduction (reduce_and_step_table); 2^25 elements = 128 MiB.
+        # None: overlapped unless the deterministic mode is on; True / False force it
+        self.table_overlap = None
         self.table_chunk = 1 << 25
         self._side = None      # prefetch stream (stage-b geometry of the next batch)
         self._pending = []     # prefetched geometries not yet consumed by train_step
@@ -405,6 +406,9 @@ class Trainer:
         full = ranges == [(0, self.model.flat.numel())]
         self._ranges_key, self._ranges = key, None if full else ranges
         return self._ranges
+
+    def _table_overlap(self):
+        return (not self.model.deterministic) if self.table_overlap is None else bool(self.table_overlap)
 
     def table_trains(self):
         """Stage a: whether the hash table is among the optimized, requires_grad parameters."""
@@ -682,7 +686,7 @@ class Trainer:
         if self.table_trains():
             # (a frozen table needs no averaged gradient: no collective for it)
             reduce_and_step_table(self.optim_table, self._grad_table, lr, eng.table16, self.world_size,
-                                  self.table_chunk, overlap=self.table_overlap and not m.deterministic)
+                                  self.table_chunk, overlap=self._table_overlap())
         self.current_iteration += 1
         self._publish(lv)
         return m.outputs(st) if return_outputs else None
@@ -716,7 +720,7 @@ class Trainer:
         if self.stage == "a" and self.table_trains():
             table = m.neural_sdf.tcnn_encoding.params
             reduce_and_step_table(self.optim_table, table.grad, self.lr(), m.engine.table16, self.world_size,
-                                  self.table_chunk, overlap=self.table_overlap and not m.deterministic)
+                                  self.table_chunk, overlap=self._table_overlap())
         self.current_iteration += 1
         self._publish(lv)
         return out

@@ -158,3 +158,77 @@ def test_stage_a_autograd_path_matches_fused():
         a, b = model.flat_grad_from_params()[off:off + n].cpu(), g_fused[off:off + n].cpu()
         assert _cos(a, b) > 0.99999 and float((a - b).norm() / b.norm().clamp_min(1e-30)) < 1e-3, name
     assert _cos(table.grad.cpu(), t_fused.cpu()) > 0.99999
+
+
+def _two_steps_a(world=1, chunk=None, overlap=True, frame=3):
+    cfg, model, trainer, sd, data, u = _setup(32, 16, 4, 100000)
+    trainer.world_size = world
+    trainer.table_overlap = overlap
+    if chunk:
+        trainer.table_chunk = chunk
+    trainer.model.deterministic = True   # bit-reproducible gradients (fixed-order sums)
+    for s in range(2):
+        b = synthetic.make_batch(32, frame=frame + 10 * s)
+        trainer.train_step({k: v.to(DEV) for k, v in b.items()}, u=u.to(DEV))
+    torch.cuda.synchronize()
+    t = model.neural_sdf.tcnn_encoding.params
+    return dict(table=t.detach().cpu().clone(), table16=model.engine.table16.cpu().clone(),
+                m=trainer.optim_table.m.cpu().clone(), v=trainer.optim_table.v.cpu().clone(),
+                flat=model.flat.detach().cpu().clone(), gtab=trainer._grad_table.cpu().clone())
+
+
+def test_table_step_chunked_equals_single_launch():
+    """The table AdamW issued chunk by chunk (the overlapped reduction's form, here at world 1
+    through FusedAdamW.step(ranges=...)) equals the single launch bit for bit."""
+    _need_gpu()
+    from mli_nerf_amd.trainer import FusedAdamW, table_chunks
+    g = torch.Generator().manual_seed(3)
+    n = 3 * (1 << 20) + 123
+    p0 = torch.randn(n, generator=g).to(DEV)
+    grads = [torch.randn(n, generator=g).to(DEV) for _ in range(3)]
+    outs = []
+    for chunked in (False, True):
+        p = p0.clone()
+        opt = FusedAdamW(p)
+        p16 = torch.empty(n, dtype=torch.float16, device=DEV)
+        for gr in grads:
+            opt.step(gr, 1e-3, p16=p16, ranges=table_chunks(n, 1 << 18) if chunked else None)
+        torch.cuda.synchronize()
+        outs.append((p.cpu(), p16.cpu(), opt.m.cpu(), opt.v.cpu()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+def _world2_worker(rank, port, results):
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        results[(rank, "overlap")] = _two_steps_a(2, chunk=1 << 16, overlap=True, frame=3 + rank)
+        results[(rank, "serial")] = _two_steps_a(2, overlap=False, frame=3 + rank)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_stage_a_world2_on_one_gpu_overlap_equals_serial():
+    """Two ranks (gloo, both on cuda:0, different rays) run two stage-a steps with the real HIP
+    engine: the overlapped chunked table reduction (chunk i's AdamW behind chunk i's all-reduce)
+    gives the same table, fp16 shadow, moments and MLP buffer as the serial single all-reduce,
+    bit for bit, and the replicas agree."""
+    _need_gpu()
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    results = ctx.Manager().dict()
+    mp.start_processes(_world2_worker, args=(port, results), nprocs=2, join=True, start_method="spawn")
+    for r in range(2):
+        for k in ("table", "table16", "m", "v", "flat", "gtab"):
+            assert torch.equal(results[(r, "overlap")][k], results[(r, "serial")][k]), (r, k)
+            assert torch.equal(results[(r, "overlap")][k], results[(0, "overlap")][k]), (r, k)
+    assert not torch.equal(results[(0, "overlap")]["table"], _two_steps_a(1)["table"])   # the ranks averaged
