@@ -10,6 +10,9 @@ from .config import merge, to_attr
 
 BASE = {
     "max_iter": 500000,                                                     # base.yaml:13
+    "max_epoch": 9999999999,                                                # imaginaire/config_base.yaml:22
+    "checkpoint": {"save_iter": 20000,                                      # base.yaml:20-21
+                   "save_latest_iter": 9999999999, "save_epoch": 9999999999},  # config_base.yaml:44-45
     "trainer": {
         "type": "mli_nerf_amd.trainer",
         "loss_weight": {"render": 1.0, "eikonal": 0.1, "curvature": 5e-4,   # syn_hotdog_b.yaml:4-9

@@ -192,6 +192,25 @@ MLI_FI void stage_flush(Stager& sg, const uint8_t* lds, int S) {
 MLI_FI float relu1(float x) {
   return __builtin_bit_cast(float, max(__builtin_bit_cast(int, x), 0));
 }
+// The ReLU mask of an accumulator tile from its ReLU outputs r = relu1(acc): bit i = (r[i] > 0)
+// = (acc[i] > 0) for every non-NaN acc.  Two VALU per element: a compare into VCC and
+// b = b + b + VCC (v_addc), elements 15 .. 0 so that element i lands in bit i; the compiler's
+// form (compare, select of 1 << i, or3) took 2.5.  The inputs are VALU results (relu1), not
+// MFMA results, so the asm needs no MFMA -> VALU wait states.
+MLI_FI uint32_t relu_bits16(const f32x16& r) {
+  uint32_t b = 0;
+#pragma unroll
+  for (int i = 15; i >= 0; --i)
+    asm("v_cmp_lt_i32 vcc, 0, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc"
+        : "+v"(b) : "v"(__builtin_bit_cast(int, r[i])) : "vcc");
+  return b;
+}
+// acc where bit `bit0 + i` of `bits` is set, else +0 (the backward's ReLU derivative): a signed
+// one-bit field extract (0 / -1) and an and, two VALU per element (the compiler's form -- and,
+// compare, select -- took three).
+MLI_FI float mask_bit(float x, uint32_t bits, int bit) {
+  return __builtin_bit_cast(float, __builtin_bit_cast(int, x) & __builtin_amdgcn_sbfe((int)bits, bit, 1));
+}
 // acc = W_chunk (32 x 16*KS) * X (16*KS x 32) + bias.  PF = 0: the compiler's schedule (it reads
 // two weight fragments ahead and waits lgkmcnt(0) before every MFMA pair, so each pair pays the
 // LDS latency); PF > 0: the fragments are read PF ahead, one read issued after each MFMA (the
@@ -513,9 +532,7 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
         out[2 * t] = acc_to_frag(v, 0);
         out[2 * t + 1] = acc_to_frag(v, 1);
         if (TRAIN) {
-          uint32_t bits = 0;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) bits |= (acc[i] > 0.0f ? 1u : 0u) << i;
+          const uint32_t bits = relu_bits16(v);
           if (t & 1) mbits[t >> 1] |= bits << 16; else mbits[t >> 1] = bits;
           if (stg)
             stage_tile<G>(sg, lds, out[2 * t], out[2 * t + 1],
@@ -653,10 +670,9 @@ MLI_FI void rgb_bwd_body(const mli_rgb_bwd_args& a, uint8_t* lds) {
             *reinterpret_cast<const u32x4*>(lds + G::MASK_OFF + (li & 1) * G::MASKB + wave * 1024 + lane * 16);
         const int wi = t >> 1;
         const uint32_t word = wi == 0 ? mv[0] : wi == 1 ? mv[1] : wi == 2 ? mv[2] : mv[3];
-        const uint32_t bits = word >> ((t & 1) * 16);
         f32x16 v;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = ((bits >> i) & 1u) ? acc[i] : 0.0f;
+        for (int i = 0; i < 16; ++i) v[i] = mask_bit(acc[i], word, (t & 1) * 16 + i);
         out[2 * t] = acc_to_frag(v, 0);
         out[2 * t + 1] = acc_to_frag(v, 1);
         stage_tile<G>(sg, lds, out[2 * t], out[2 * t + 1],

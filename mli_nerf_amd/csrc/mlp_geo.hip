@@ -72,10 +72,9 @@ __global__ __launch_bounds__(GGeo::THREADS) void geo_bwd_kernel(mli_geo_bwd_args
           *reinterpret_cast<const u32x4*>(lds + G::MASK_OFF + (li & 1) * G::MASKB + wave * 1024 + lane * 16);
       const int wi = t >> 1;
       const uint32_t word = wi == 0 ? mv[0] : wi == 1 ? mv[1] : wi == 2 ? mv[2] : mv[3];
-      const uint32_t bits = word >> ((t & 1) * 16);
       f32x16 v;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = ((bits >> i) & 1u) ? acc[i] : 0.0f;
+      for (int i = 0; i < 16; ++i) v[i] = mask_bit(acc[i], word, (t & 1) * 16 + i);
       out[2 * t] = acc_to_frag(v, 0);
       out[2 * t + 1] = acc_to_frag(v, 1);
       stage_tile<G>(sg, lds, out[2 * t], out[2 * t + 1], a.dzT + ((size_t)layer * 256 + 32 * t) * S + col0, lane);

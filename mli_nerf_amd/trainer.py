@@ -861,6 +861,39 @@ class Trainer:
             self.optim_table.resize(self.model.neural_sdf.tcnn_encoding.params.numel())
         return res
 
+    # ------------------------------------------------------------ train.py / test.py surface
+    # (mli_nerf_amd.loop: the imaginaire loop reduced to the hot path; W&B is out of scope)
+    train_data_loader = eval_data_loader = None
+
+    def set_data_loader(self, cfg, split, shuffle=True, drop_last=True, seed=0, subset_indices=None):
+        """imaginaire/trainers/base.py:87-101 (train.py:81-82, test.py:104-116)."""
+        from . import loop
+        loop.set_data_loader(self, cfg, split, shuffle, drop_last, seed, subset_indices)
+
+    def init_wandb(self, cfg, wandb_id=None, project="", run_name=None, mode="online", resume="allow",
+                   use_group=False):
+        """base.py:231-272 (train.py:86-90): W&B is not part of this build: recorded only."""
+        self.wandb_args = dict(project=project, run_name=run_name, mode=mode, resume=resume)
+
+    def train(self, cfg, data_loader, single_gpu=False, profile=False, show_pbar=False):
+        """base.py:474-527 + neuralangelo/trainer.py:110-112 (train.py:94-98)."""
+        from . import loop
+        loop.train(self, cfg, data_loader, single_gpu, profile, show_pbar)
+
+    def finalize(self, cfg):
+        """base.py:551-554 (train.py:101): closes the W&B run in the reference; nothing to close here."""
+        return None
+
+    def test_save(self, data_loader, output_dir=None, inference_args=None, mode="test", show_pbar=False):
+        """projects/nerf/trainers/base.py:176-216 (test.py:119-121)."""
+        from . import loop
+        return loop.test_save(self, data_loader, output_dir, inference_args, mode, show_pbar)
+
+    def test_images(self, data_loader, output_dir=None, setting_list=None, mode="test", show_pbar=False):
+        """projects/nerf/trainers/base.py:218-260 (test.py:122-126)."""
+        from . import loop
+        return loop.test_images(self, data_loader, output_dir, setting_list, mode, show_pbar)
+
     def test_video(self, data_loader, setting1, setting2, output_dir, mode="test",
                    video_content=("rgb", "gt", "o_r", "o_s"), show_pbar=False):
         """projects/nerf/trainers/base.py:264-346 (see mli_nerf_amd.video); ``data_loader`` as
