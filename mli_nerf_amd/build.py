@@ -10,7 +10,7 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmli_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["rays.hip", "sdf.hip", "mlp_fwd.hip", "mlp_fwd_pq.hip", "mlp_fwd_train.hip", "mlp_fwd_w64.hip", "mlp_bwd.hip", "mlp_geo.hip",
+SOURCES = ["rays.hip", "sdf.hip", "mlp_fwd.hip", "mlp_fwd_pq.hip", "mlp_fwd_train.hip", "mlp_bwd.hip", "mlp_geo.hip",
            "wgrad.hip", "params.hip", "loss.hip"]
 # sdf.hip: no SLP packing, so fma(fp16 -> fp32 feature, w, acc) selects v_fma_mix_f32 (one
 # instruction) instead of v_cvt_f32_f16 x2 + v_pk_fma_f32
@@ -70,8 +70,9 @@ def build(verbose=False, extra=(), out=None):
     digest = source_hash()
     if not extra and built_hash(out) == digest:  # built from exactly these sources and flags
         return out
-    with cf.ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
-        results = list(ex.map(lambda s: _compile(s, extra, tag, digest), SOURCES))
+    srcs = SOURCES + (["mlp_fwd_w64.hip"] if "-DMLI_EXP_W64" in extra else [])  # (round-4 experiment)
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        results = list(ex.map(lambda s: _compile(s, extra, tag, digest), srcs))
     if verbose:
         for _, log in results:
             if log:

@@ -16,11 +16,11 @@ extern "C" int mli_rgb_fwd(const mli_rgb_fwd_args* a, mli_stream_t s) {
   if (pq && (!train || a->q4 == nullptr || a->N % 32 != 0)) return (int)hipErrorInvalidValue;
   if (!pq && a->q4 != nullptr) return (int)hipErrorInvalidValue;
   const dim3 grid(S / GFwd::SAMPLES), block(GFwd::THREADS);
+#ifdef MLI_EXP_W64
+  if (getenv("MLI_W64") && (pq || !train)) return mli_launch_rgb_fwd_w64(a, (hipStream_t)s, atoi(getenv("MLI_W64")));
+#endif
   if (pq) return mli_launch_rgb_fwd_pq(a, (hipStream_t)s);
   if (train) return mli_launch_rgb_fwd_train(a, (hipStream_t)s);
-#ifdef MLI_EXP_W64
-  if (getenv("MLI_W64")) return mli_launch_rgb_fwd_w64(a, (hipStream_t)s, atoi(getenv("MLI_W64")));
-#endif
   static_assert(GFwd::LDS_FWD_F <= 163840, "LDS per workgroup");
   hipLaunchKernelGGL((rgb_fwd_kernel<false, false>), grid, block, GFwd::LDS_FWD_F, (hipStream_t)s, *a);
   MLI_LAUNCH_CHECK();
