@@ -70,9 +70,8 @@ def build(verbose=False, extra=(), out=None):
     digest = source_hash()
     if not extra and built_hash(out) == digest:  # built from exactly these sources and flags
         return out
-    srcs = SOURCES + (["mlp_fwd_w64.hip"] if "-DMLI_EXP_W64" in extra else [])  # (round-4 experiment)
-    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        results = list(ex.map(lambda s: _compile(s, extra, tag, digest), srcs))
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
+        results = list(ex.map(lambda s: _compile(s, extra, tag, digest), SOURCES))
     if verbose:
         for _, log in results:
             if log:

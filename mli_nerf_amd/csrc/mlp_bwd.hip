@@ -1,9 +1,5 @@
 // Heads backward dX chain (the shared heads machinery: mlp_core.h).
 #include "mlp_core.h"
-#ifdef MLI_EXP_W64
-#include <stdlib.h>
-int mli_launch_rgb_bwd_w64(const mli_rgb_bwd_args* a, hipStream_t s, int variant);
-#endif
 
 namespace {
 
@@ -19,9 +15,6 @@ __global__ __launch_bounds__(GBwd::THREADS) void rgb_bwd_kernel(mli_rgb_bwd_args
 extern "C" int mli_rgb_bwd(const mli_rgb_bwd_args* a, mli_stream_t s) {
   const int S = a->R * a->N;
   if (S % 256 != 0) return (int)hipErrorInvalidValue;
-#ifdef MLI_EXP_W64
-  if (getenv("MLI_W64B")) return mli_launch_rgb_bwd_w64(a, (hipStream_t)s, atoi(getenv("MLI_W64B")));
-#endif
   hipLaunchKernelGGL(rgb_bwd_kernel, dim3(S / GBwd::SAMPLES), dim3(GBwd::THREADS), GBwd::LDS_BWD, (hipStream_t)s,
                      *a);
   MLI_LAUNCH_CHECK();

@@ -197,12 +197,14 @@ MLI_FI float relu1(float x) {
 // b = b + b + VCC (v_addc), elements 15 .. 0 so that element i lands in bit i; the compiler's
 // form (compare, select of 1 << i, or3) took 2.5.  The inputs are VALU results (relu1), not
 // MFMA results, so the asm needs no MFMA -> VALU wait states.
+// (the element goes through a float parameter: __builtin_bit_cast of a vector element expression
+// reads element 0 -- every compare then saw the same value)
+MLI_FI int f32_bits(float x) { return __builtin_bit_cast(int, x); }
 MLI_FI uint32_t relu_bits16(const f32x16& r) {
   uint32_t b = 0;
 #pragma unroll
   for (int i = 15; i >= 0; --i)
-    asm("v_cmp_lt_i32 vcc, 0, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc"
-        : "+v"(b) : "v"(__builtin_bit_cast(int, r[i])) : "vcc");
+    asm("v_cmp_lt_i32 vcc, 0, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(b) : "v"(f32_bits(r[i])) : "vcc");
   return b;
 }
 // acc where bit `bit0 + i` of `bits` is set, else +0 (the backward's ReLU derivative): a signed
@@ -302,6 +304,51 @@ struct NoPre {
   MLI_FI int count(int) const { return 0; }
   MLI_FI void issue(int) const {}
 };
+
+// run_layer with the epilogue deferred by one tile (DEFER): phase t issues the MFMA chain of tile
+// t, then epi(t - 1) on the accumulators carried across the barrier (pacc), so the wave's own
+// epilogue VALU / LDS work has the chain's MFMAs to hide behind instead of following them.  The
+// last tile's epilogue is the caller's: the next layer runs it as `prev` at its first phase,
+// before its chain in program order (it produces that chain's last k-steps).  Flushes follow the
+// stager at run time (a tile staged in phase t leaves in phase t + 1); the static store counts of
+// the vmcnt waits count only what is known to be issued after the chunk being retired (EPI
+// stores of epi(t - 1)); undercounting only waits longer.
+// MASKN: stores of the last tile's epilogue beyond EPI (the ReLU mask image); PREVN: stores that
+// prev issues (the previous layer's deferred last tile: its mask store).
+template <class G, int ROLE, int KS, int NT, int EPI, int MASKN, int PREVN, bool DEFER, class Bytes, class Pre,
+          class Prev, class Epi>
+MLI_FI void run_layer_d(Ring& rg, uint8_t* lds, Stager& sg, int S, const half8* X, int lane, Bytes&& bytes,
+                        Pre&& pre, Prev&& prev, Epi&& epi, f32x16& pacc) {
+  static_assert(ROLE != ALL, "split wave roles only (the flushes are not counted)");
+  auto stores = [](int t) MLI_LAMBDA_FI {
+    if (t < 0) return 0;
+    const int pv = t == 0 ? PREVN : 0;
+    if (DEFER) return pv + (t >= 1 ? EPI : 0);
+    return pv + EPI + (t == NT - 1 ? MASKN : 0);
+  };
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    pre.issue(t);
+    ring_issue<G, ROLE>(rg, lds, bytes);
+    if (ROLE != DMA && sg.pend) stage_flush<G, ROLE>(sg, lds, S);
+    if (t == 0) prev(pacc);
+    const f32x16 acc = chunk_mma<KS, G::PF>(lds + (rg.cur % NSLOT) * G::SLOT, X, lane);
+    if (DEFER) {
+      if (t > 0) epi(t - 1, pacc);
+      pacc = acc;
+    } else {
+      epi(t, acc);
+    }
+    if (ROLE != STORE) vm_wait((DIST - 1) * G::template ring_ops<ROLE>() + pre.count(t) + stores(t) + stores(t - 1));
+    block_sync();
+    rg.cur++;
+  }
+}
+
+// The heads kernels defer every layer's epilogue by one tile.  Measured (profiles/r4/defer2,
+// alternating on one box): step 4.29 / 4.30 -> 4.25 / 4.24 ms, rgb_fwd 1.150 -> 1.108-1.128 ms,
+// rgb_bwd 0.926 -> 0.914-0.920 ms against the same kernels with the epilogue in place; bit-identical.
+constexpr bool HEADS_DEFER = true;
 
 // ---------------------------------------------------------------------- output-layer partials
 // PQ mode (stage b): the output layer's weight gradient factors through the per-ray loss
@@ -490,8 +537,9 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
 
   // SDF layer 1: feat = softplus(W1 h0 + b1) -> A; frag image scratch (+ x0T rows 0..255)
   uint16_t* ftile = a.feat_frag + (size_t)tile * FRAG_TILE;
-  run_layer<G, ROLE, 16, 8, TRAIN, 2, false>(rg, lds, sg, S, B, lane, bytes, NoPre{},
-                                    [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
+  f32x16 pacc;  // (HEADS_DEFER: the accumulators of the tile whose epilogue is pending)
+  auto none = [](f32x16&) MLI_LAMBDA_FI {};
+  auto feat_epi = [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
     f32x16 v;
 #pragma unroll
     for (int i = 0; i < 16; i += 2) {
@@ -510,7 +558,15 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
       fl[64] = A[2 * t + 1];
     }
     if (TRAIN) stage_tile<G>(sg, lds, A[2 * t], A[2 * t + 1], a.x0T + (size_t)(32 * t) * S + col0, lane);
-  });
+  };
+  run_layer_d<G, ROLE, 16, 8, 2, 0, 0, HEADS_DEFER>(rg, lds, sg, S, B, lane, bytes, NoPre{}, none, feat_epi, pacc);
+  if (HEADS_DEFER) {
+    // the last feat tile, before the heads reload feat: tile 6's staged x0T rows leave first,
+    // tile 7's are made visible for the next phase's flush
+    if (TRAIN && ROLE != DMA && sg.pend) stage_flush<G, ROLE>(sg, lds, S);
+    feat_epi(7, pacc);
+    if (TRAIN) block_sync();
+  }
 
   for (int hd = 0; hd < a.n_heads; ++hd) {
     const int S = opaque_s(a.R * a.N);
@@ -545,16 +601,26 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
         }
       };
     };
-    run_layer<G, ROLE, 19, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, B, lane, bytes, NoPre{}, relu_epi(A, 0, true));
-    run_layer<G, ROLE, 16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, A, lane, bytes, NoPre{}, relu_epi(B, 1, true));
-    run_layer<G, ROLE, 16, 8, TRAIN, 0, TRAIN>(rg, lds, sg, S, B, lane, bytes, NoPre{}, relu_epi(A, 2, true));
-    run_layer<G, ROLE, 16, 8, TRAIN && !PQ, 0, TRAIN>(rg, lds, sg, S, A, lane, bytes, NoPre{},
-                                                      relu_epi(B, 3, !PQ));
+    auto e0 = relu_epi(A, 0, true);
+    auto e1 = relu_epi(B, 1, true);
+    auto e2 = relu_epi(A, 2, true);
+    auto e3 = relu_epi(B, 3, !PQ);
+    // (deferred: layer l's last tile is finished by layer l + 1's first phase)
+    auto fin = [&](auto& e) MLI_LAMBDA_FI {
+      return [&](f32x16& p) MLI_LAMBDA_FI {
+        if (HEADS_DEFER) e(7, p);
+      };
+    };
+    constexpr int MN = TRAIN ? 1 : 0, PN = TRAIN && HEADS_DEFER ? 1 : 0;
+    run_layer_d<G, ROLE, 19, 8, 0, MN, 0, HEADS_DEFER>(rg, lds, sg, S, B, lane, bytes, NoPre{}, none, e0, pacc);
+    run_layer_d<G, ROLE, 16, 8, 0, MN, PN, HEADS_DEFER>(rg, lds, sg, S, A, lane, bytes, NoPre{}, fin(e0), e1, pacc);
+    run_layer_d<G, ROLE, 16, 8, 0, MN, PN, HEADS_DEFER>(rg, lds, sg, S, B, lane, bytes, NoPre{}, fin(e1), e2, pacc);
+    run_layer_d<G, ROLE, 16, 8, 0, MN, PN, HEADS_DEFER>(rg, lds, sg, S, A, lane, bytes, NoPre{}, fin(e2), e3, pacc);
     const int no = hd == 2 ? 1 : 3;
     const int off = hd * 3;
     float gq[3] = {0.f, 0.f, 0.f};
-    run_layer<G, ROLE, 16, 1, false, 0, false>(rg, lds, sg, S, B, lane, bytes, NoPre{},
-                                      [&](int, const f32x16& acc) MLI_LAMBDA_FI {
+    run_layer_d<G, ROLE, 16, 1, 0, 0, PN, false>(rg, lds, sg, S, B, lane, bytes, NoPre{}, fin(e3),
+                                          [&](int, const f32x16& acc) MLI_LAMBDA_FI {
       if (h == 0) {
 #pragma unroll
         for (int i = 0; i < 3; ++i)
@@ -564,10 +630,12 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
             if (PQ) gq[i] = Q4_SCALE * wgt * (y * (1.0f - y));
           }
       }
-    });
+    }, pacc);
     // (the q4 stores come from the STORE waves only: the DMA waves' counted waits are unchanged)
     if (PQ) q4_tile<G, ROLE>(a, lds, B, gq, hd, lane);
   }
+  // (training without PQ: X3's last tile is still staged)
+  if (ROLE != DMA && sg.pend) stage_flush<G, ROLE>(sg, lds, opaque_s(a.R * a.N));
   vm_wait(0);  // no LDS-DMA may land after the workgroup's LDS is released
 }
 
@@ -679,10 +747,28 @@ MLI_FI void rgb_bwd_body(const mli_rgb_bwd_args& a, uint8_t* lds) {
                       a.dzT + ((size_t)(hd * 4 + layer) * 256 + 32 * t) * S + col0, lane);
       };
     };
-    run_layer<G, ROLE, 1, 8, true, 0, false>(rg, lds, sg, S, &z4, lane, bytes, pre(0), mask_epi(A, 3, 0));
-    run_layer<G, ROLE, 16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, pre(1), mask_epi(B, 2, 1));
-    run_layer<G, ROLE, 16, 8, true, 0, false>(rg, lds, sg, S, B, lane, bytes, pre(2), mask_epi(A, 1, 2));
-    run_layer<G, ROLE, 16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, pre(3), mask_epi(B, 0, 3));
+    auto e3 = mask_epi(A, 3, 0);
+    auto e2 = mask_epi(B, 2, 1);
+    auto e1 = mask_epi(A, 1, 2);
+    auto e0 = mask_epi(B, 0, 3);
+    auto none = [](f32x16&) MLI_LAMBDA_FI {};
+    auto fin = [&](auto& e) MLI_LAMBDA_FI {
+      return [&](f32x16& p) MLI_LAMBDA_FI {
+        if (HEADS_DEFER) e(7, p);
+      };
+    };
+    f32x16 pacc;
+    run_layer_d<G, ROLE, 1, 8, 0, 0, 0, HEADS_DEFER>(rg, lds, sg, S, &z4, lane, bytes, pre(0), none, e3, pacc);
+    run_layer_d<G, ROLE, 16, 8, 0, 0, 0, HEADS_DEFER>(rg, lds, sg, S, A, lane, bytes, pre(1), fin(e3), e2, pacc);
+    run_layer_d<G, ROLE, 16, 8, 0, 0, 0, HEADS_DEFER>(rg, lds, sg, S, B, lane, bytes, pre(2), fin(e2), e1, pacc);
+    run_layer_d<G, ROLE, 16, 8, 0, 0, 0, HEADS_DEFER>(rg, lds, sg, S, A, lane, bytes, pre(3), fin(e1), e0, pacc);
+    if (HEADS_DEFER) {
+      // the head's last tile: tile 6 (staged by the last phase) leaves first, then tile 7 is
+      // staged and made visible for the next phase's flush
+      if (ROLE != DMA && sg.pend) stage_flush<G, ROLE>(sg, lds, S);
+      e0(7, pacc);
+      block_sync();
+    }
   }
   // the last tile, made visible by the last phase's barrier
   stage_flush<G, ROLE>(sg, lds, opaque_s(a.R * a.N));

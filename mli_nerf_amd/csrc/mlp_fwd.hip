@@ -1,9 +1,5 @@
 // Heads forward: the C entry points and the eval kernel (the shared heads machinery: mlp_core.h).
 #include "mlp_core.h"
-#ifdef MLI_EXP_W64
-#include <stdlib.h>
-int mli_launch_rgb_fwd_w64(const mli_rgb_fwd_args* a, hipStream_t s, int variant);
-#endif
 
 extern "C" int mli_rgb_fwd(const mli_rgb_fwd_args* a, mli_stream_t s) {
   const int S = a->R * a->N;
@@ -16,9 +12,6 @@ extern "C" int mli_rgb_fwd(const mli_rgb_fwd_args* a, mli_stream_t s) {
   if (pq && (!train || a->q4 == nullptr || a->N % 32 != 0)) return (int)hipErrorInvalidValue;
   if (!pq && a->q4 != nullptr) return (int)hipErrorInvalidValue;
   const dim3 grid(S / GFwd::SAMPLES), block(GFwd::THREADS);
-#ifdef MLI_EXP_W64
-  if (getenv("MLI_W64") && (pq || !train)) return mli_launch_rgb_fwd_w64(a, (hipStream_t)s, atoi(getenv("MLI_W64")));
-#endif
   if (pq) return mli_launch_rgb_fwd_pq(a, (hipStream_t)s);
   if (train) return mli_launch_rgb_fwd_train(a, (hipStream_t)s);
   static_assert(GFwd::LDS_FWD_F <= 163840, "LDS per workgroup");

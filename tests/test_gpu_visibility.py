@@ -85,8 +85,11 @@ def test_light_visibility_matches_oracle(config):
     check("inter_dist mean abs", err.mean().item(), 2e-4, "<=")
     check("inter_dist max abs", err.max().item(), 1e-2, "<=")
     # the shading terms are the 4-tap normal at the traced intersection (inter_dist above: <= 1e-2
-    # apart) dotted with the light: 2e-3 (measured 0.4-1.1e-3; fp32 pre-activation rounding, fma
-    # vs mul + add, moves the 1.8e3x-amplified tap differences by that much)
+    # apart) dotted with the light.  Measured (round 4, profiles/r4/suite/margins.json): p99 of
+    # |GPU - oracle| 3.3e-4 (normal_x_light) and 3.0e-4 (pseudo_shading), max 1.11e-3 and 7.6e-4
+    # over both cases -- a handful of grazing hits, where the 4-tap normal (sdf differences / 5.6e-4:
+    # the fp16-operand sdf error amplified 1.8e3x) moves most.  So the bulk is held at 1e-3 (p99)
+    # and the tail at 2e-3 (max); round 3's failed 1e-3 max bar was the tail (1.11e-3).
     for k in ("normal_x_light", "pseudo_shading"):
         e = (g[k] - ref[k]).abs()[both]
         check(k + " p99 abs", torch.quantile(e, 0.99).item(), 1e-3, "<=")
