@@ -150,7 +150,6 @@ def run_infer(args, world, rank, dev):
     model = Model(cfg.model, cfg.data)
     model.load_state_dict(synthetic.make_state_dict(log2T=22, seed=0))
     model = model.to(dev)
-    model.field_one_pass = args.field == "one"
     N = model.pcfg.n_samples
     frames = [{k: v.to(dev) for k, v in synthetic.make_batch(1, H=size, W=size, frame=f).items()}
               for f in range(args.warmup + args.frames)]
@@ -531,8 +530,6 @@ def main(argv=None):
                     help="stage-b output-layer dW: on = per-tile partials formed in the heads forward "
                          "(mli_rgb_fwd PQ mode + mli_dw4; X3 never written), off = X3 through HBM and the "
                          "THIN split-K class")
-    ap.add_argument("--field", choices=("one", "two"), default="two",
-                    help="FIELD in one pass (no encoding image; stage b / inference) or the two-phase kernels")
     ap.add_argument("--mode", choices=("train", "infer"), default="train",
                     help="train: BASELINE configs[1] step; infer: configs[4] full-frame render")
     ap.add_argument("--frames", type=int, default=4, help="infer: frames timed (after --warmup frames)")
@@ -582,7 +579,6 @@ def main(argv=None):
     trainer = Trainer(cfg, is_inference=False, model=model, world_size=world)
     trainer.fused_tail = args.tail == "fused"
     model.pq = args.pq == "on"
-    model.field_one_pass = args.field == "one"
     if stage_a:
         # steady state of stage a: past the coarse-to-fine ramp (all 16 levels active)
         trainer.current_iteration = args.iteration

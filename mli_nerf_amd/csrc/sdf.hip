@@ -413,226 +413,6 @@ __global__ __launch_bounds__(MLP_WAVES * 64) void field_mlp_kernel(mli_sdf_args 
   }
 }
 
-// ---------------------------------------------------------------- FIELD mode, one pass
-// Without an encoding image (stage b, inference: nothing re-reads the encodings) the two
-// phases run in one workgroup as producer and consumer through LDS.  Waves 0-7 gather: wave
-// w runs level pair w of the round's tile (level5, the same code and arithmetic as
-// encode5_kernel) into an LDS slot holding the tile's 5 x 8 B-fragments (40 KiB).  Waves 8-11
-// run layer 0 + softplus + the sdf dot on the previous round's slot, wave 8 + u owning the
-// n-tiles 2u and 2u + 1 (their 16 weight fragments stay in registers); the four per-wave sdf
-// partials meet in LDS and wave 8 finishes the tile one round later (outside, grad, hess).
-// One s_barrier per round; the slots alternate.  The encodings and h0 are bit-identical to
-// the two-phase path; the sdf dot sums the n-tile pairs' partials instead of one chain over
-// the 8 n-tiles (float rounding only).
-constexpr int FF_GW = 8, FF_MW = 4, FF_WAVES = FF_GW + FF_MW;
-constexpr int FF_SLOT = TAPS * 8 * 1024;
-constexpr int FF_ROWC = 0;                       // 5 row-constant arrays + b_sdf (5136 B)
-constexpr int FF_SLOTS = 6144;                   // 2 slots
-constexpr int FF_JOBS = FF_SLOTS + 2 * FF_SLOT;  // 8 job lists of 4 x 64 TapJobs
-constexpr int FF_RED = FF_JOBS + FF_GW * 4 * 64 * (int)sizeof(TapJob);  // 2 x [5][4][32] fp32
-constexpr int FF_LDS = FF_RED + 2 * TAPS * FF_MW * 32 * 4;
-static_assert(5 * ROWC_ARRAY + 16 <= FF_SLOTS, "ff rowc");
-static_assert(FF_LDS <= 160 * 1024, "ff lds");
-
-// Sample of lane c in tile `tile` (clamped past the end, as field_mlp_kernel).
-struct FfSample {
-  int slot, r;
-  bool valid;
-};
-MLI_FI FfSample ff_sample(const mli_sdf_args& a, int tile, int c) {
-  const int n_total = a.R * a.n_per_ray;
-  const int m = tile * 32 + c;
-  const bool valid = m < n_total;
-  const int mm = valid ? m : n_total - 1;
-  const int r = mm / a.n_per_ray, k = mm - r * a.n_per_ray;
-  return FfSample{k * a.R + r, r, valid};
-}
-
-// Producer: level pair qq of the 5 points of `tile` into the slot.
-MLI_FI void ff_gather(const mli_sdf_args& a, uint8_t* slotp, TapJob* jobs, int tile, int qq, int lane) {
-  const FfSample sm = ff_sample(a, tile, lane & 31);
-  float q[TAPS][3];
-  field_points(a, sm.slot, sm.r, q);
-  float x[TAPS][3];
-#pragma unroll
-  for (int p = 0; p < TAPS; ++p)
-#pragma unroll
-    for (int d = 0; d < 3; ++d) x[p][d] = (q[p][d] + 2.0f) * 0.25f;  // modules.py:82-83
-  uint8_t* dst = slotp + qq * 1024;
-  const int lv0 = 2 * qq, lv1 = 2 * qq + 1;
-  if (lv0 >= a.active_levels) {  // coarse-to-fine: the whole level pair encodes to 0
-#pragma unroll
-    for (int p = 0; p < TAPS; ++p) *reinterpret_cast<u32x4*>(dst + p * 8 * 1024 + lane * 16) = u32x4{0, 0, 0, 0};
-    return;
-  }
-  const mli_grid_levels& L = a.levels;
-  const LevelP P0 = level_params(L, lv0), P1 = level_params(L, lv1);
-  const bool keep0 = lv0 < a.active_levels, keep1 = lv1 < a.active_levels;
-  const bool d0 = level_dense(L, lv0), d1 = level_dense(L, lv1);
-  auto sink = [&](int p, int src, const half8& e) MLI_LAMBDA_FI {
-    *reinterpret_cast<half8*>(dst + p * 8 * 1024 + src * 16) = e;
-  };
-  if (d0 && d1)
-    level5<0>(a.table, P0, P1, lane, x, keep0, keep1, jobs, sink);
-  else if (!d0 && !d1)
-    level5<1>(a.table, P0, P1, lane, x, keep0, keep1, jobs, sink);
-  else
-    level5<2>(a.table, P0, P1, lane, x, keep0, keep1, jobs, sink);
-}
-
-// Consumer: n-tiles 2u, 2u + 1 of layer 0 for the 5 points of `tile` (h0 k-steps 4u..4u+3 of
-// the center), the pair's sdf partials into red[5][4][32].
-MLI_FI void ff_mlp(const mli_sdf_args& a, const uint8_t* lds, const uint8_t* slotp, float* red, int u,
-                   const half8 (&w)[2][8], int tile, int lane) {
-  const int c = lane & 31, h = lane >> 5;
-  const FfSample sm = ff_sample(a, tile, c);
-  // the center p = c + v d (field_points; the taps p + k_i eps are rebuilt per point below)
-  const float d = a.dists[sm.slot];
-  const float cx = __fadd_rn(a.center[3 * sm.r + 0], __fmul_rn(a.ray_unit[3 * sm.r + 0], d));
-  const float cy = __fadd_rn(a.center[3 * sm.r + 1], __fmul_rn(a.ray_unit[3 * sm.r + 1], d));
-  const float cz = __fadd_rn(a.center[3 * sm.r + 2], __fmul_rn(a.ray_unit[3 * sm.r + 2], d));
-  uint16_t* h0_tile = a.h0 + (size_t)tile * (16 * 64 * 8);
-  const half8* encp = reinterpret_cast<const half8*>(slotp) + lane;
-  constexpr int A4 = ROWC_ARRAY / 16;
-  const f32x4* rc0 = reinterpret_cast<const f32x4*>(lds + FF_ROWC + (4 * u + h) * 64);  // n-tile 2u
-  const f32x4* rc1 = rc0 + 8;                                                            // n-tile 2u + 1
-#pragma unroll 1
-  for (int pi = 0; pi < TAPS; ++pi) {
-    const float e = a.eps;
-    const float ex = (pi == 1 || pi == 4) ? e : -e;
-    const float ey = (pi == 3 || pi == 4) ? e : -e;
-    const float ez = (pi == 2 || pi == 4) ? e : -e;
-    const float px = pi ? __fadd_rn(cx, ex) : cx;
-    const float py = pi ? __fadd_rn(cy, ey) : cy;
-    const float pz = pi ? __fadd_rn(cz, ez) : cz;
-    f32x16 acc[2];
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {
-      const f32x4* rc = tt ? rc1 : rc0;
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const f32x4 b0 = rc[v], wx = rc[A4 + v], wy = rc[2 * A4 + v], wz = rc[3 * A4 + v];
-#pragma unroll
-        for (int j = 0; j < 4; j += 2) {
-          const f32x2 pv = pterm_x2((f32x2){b0[j], b0[j + 1]}, (f32x2){wx[j], wx[j + 1]},
-                                    (f32x2){wy[j], wy[j + 1]}, (f32x2){wz[j], wz[j + 1]}, px, py, pz);
-          acc[tt][4 * v + j] = pv.x;
-          acc[tt][4 * v + j + 1] = pv.y;
-        }
-      }
-    }
-    // k-step outer: one encoding fragment live, both n-tiles' chains in the k order of
-    // sdf_from_enc
-#pragma unroll
-    for (int qq = 0; qq < 8; ++qq) {
-      const half8 en = encp[(pi * 8 + qq) * 64];
-      acc[0] = mfma32(w[0][qq], en, acc[0]);
-      acc[1] = mfma32(w[1][qq], en, acc[1]);
-    }
-    f32x2 part2 = {0.0f, 0.0f};
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {
-      const f32x4* rc = tt ? rc1 : rc0;
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const f32x4 ws = rc[4 * A4 + v];
-#pragma unroll
-        for (int j = 0; j < 4; j += 2) {
-          const f32x2 sv = softplus100x2((f32x2){acc[tt][4 * v + j], acc[tt][4 * v + j + 1]});
-          acc[tt][4 * v + j] = sv.x;
-          acc[tt][4 * v + j + 1] = sv.y;
-          part2 = __builtin_elementwise_fma((f32x2){ws[j], ws[j + 1]}, sv, part2);
-        }
-      }
-      if (pi == 0) {  // read by the heads kernel only: non-temporal
-        half8* dst = reinterpret_cast<half8*>(h0_tile) + (2 * (2 * u + tt)) * 64 + lane;
-        __builtin_nontemporal_store(acc_to_frag(acc[tt], 0), dst);
-        __builtin_nontemporal_store(acc_to_frag(acc[tt], 1), dst + 64);
-      }
-    }
-    float part = part2.x + part2.y;
-    part += __shfl_xor(part, 32);
-    if (h == 0) red[(pi * FF_MW + u) * 32 + c] = part;
-  }
-}
-
-// The tile's sdf = the n-tile pairs' partials in order + b_sdf; outside, grad, hess as
-// field_mlp_kernel.
-MLI_FI void ff_finish(const mli_sdf_args& a, const uint8_t* lds, const float* red, int tile, int lane) {
-  if (lane >= 32) return;
-  const FfSample sm = ff_sample(a, tile, lane);
-  if (!sm.valid) return;
-  const float bsdf = *reinterpret_cast<const float*>(lds + FF_ROWC + 5 * ROWC_ARRAY);
-  float s[TAPS];
-#pragma unroll
-  for (int pi = 0; pi < TAPS; ++pi) {
-    const float* rp = red + pi * FF_MW * 32 + lane;
-    s[pi] = (((rp[0] + rp[32]) + rp[64]) + rp[96]) + bsdf;
-  }
-  float s0 = s[0];
-  const float s1 = s[1], s2 = s[2], s3 = s[3], s4 = s[4];
-  if (a.outside[sm.r]) s0 = a.outside_val;
-  const int slot = sm.slot;
-  a.sdf[slot] = s0;
-  const float gx = __fadd_rn(__fadd_rn(__fadd_rn(s1, -s2), -s3), s4);
-  const float gy = __fadd_rn(__fadd_rn(__fadd_rn(-s1, -s2), s3), s4);
-  const float gz = __fadd_rn(__fadd_rn(__fadd_rn(-s1, s2), -s3), s4);
-  a.grad[3 * slot + 0] = gx / a.grad_den;
-  a.grad[3 * slot + 1] = gy / a.grad_den;
-  a.grad[3 * slot + 2] = gz / a.grad_den;
-  if (a.with_hessian) {
-    const float sum = __fadd_rn(__fadd_rn(__fadd_rn(s1, s2), s3), s4);
-    const float hxx = __fadd_rn(sum / 2.0f, -__fmul_rn(2.0f, s0)) / a.hess_den;
-    const float hv = hxx / 3.0f;
-    a.hess[3 * slot + 0] = hv;
-    a.hess[3 * slot + 1] = hv;
-    a.hess[3 * slot + 2] = hv;
-  }
-}
-
-// Workgroup b runs tiles [b * tpw, (b + 1) * tpw) (clamped): rounds i = 0 .. n + 1 gather tile
-// i, run the MLP of tile i - 1 and finish tile i - 2.  Short-lived workgroups (tpw tiles), so the
-// heads kernels beside the prefetch get CUs back as the launch proceeds.
-__global__ __launch_bounds__(FF_WAVES * 64) void field_fused_kernel(mli_sdf_args a, int tpw) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n_total = a.R * a.n_per_ray;
-  const int tiles = (n_total + 31) >> 5;
-  const int t0 = blockIdx.x * tpw;
-  const int n = min(tiles - t0, tpw);
-  {  // row constants + b_sdf
-    const u32x4* src = reinterpret_cast<const u32x4*>(reinterpret_cast<const uint8_t*>(a.wsdf) + ROWC_OFF);
-    for (int i = tid; i < (5 * ROWC_ARRAY + 16) / 16; i += FF_WAVES * 64)
-      reinterpret_cast<u32x4*>(lds + FF_ROWC)[i] = src[i];
-  }
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(lds + FF_RED);
-  // the two roles in separate loops with one s_barrier per round each (the weight registers
-  // are live only in the consumer's loop)
-  if (wave < FF_GW) {
-    TapJob* jobs = reinterpret_cast<TapJob*>(lds + FF_JOBS) + wave * 4 * 64;
-    for (int i = 0; i < n + 2; ++i) {
-      if (i < n) ff_gather(a, lds + FF_SLOTS + (i & 1) * FF_SLOT, jobs, t0 + i, wave, lane);
-      block_sync();
-    }
-  } else {
-    const int u = wave - FF_GW;
-    half8 w[2][8];
-    const half8* wf = reinterpret_cast<const half8*>(a.wsdf) + lane;
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-      for (int qq = 0; qq < 8; ++qq) w[tt][qq] = wf[((2 * u + tt) * 8 + qq) * 64];
-    for (int i = 0; i < n + 2; ++i) {
-      if (u == 0 && i >= 2) ff_finish(a, lds, red + (i & 1) * TAPS * FF_MW * 32, t0 + i - 2, lane);
-      if (i >= 1 && i <= n)
-        ff_mlp(a, lds, lds + FF_SLOTS + ((i - 1) & 1) * FF_SLOT, red + ((i - 1) & 1) * TAPS * FF_MW * 32, u, w,
-               t0 + i - 1, lane);
-      block_sync();
-    }
-  }
-}
-
 // SDF only (sampling rounds): one point per lane, encode + layer 0 + sdf head fused.
 __global__ __launch_bounds__(256) void sdf_kernel(mli_sdf_args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -1370,15 +1150,7 @@ extern "C" int mli_sdf(const mli_sdf_args* a, mli_stream_t s) {
     MLI_LAUNCH_CHECK();
   }
   if (a->h0 == nullptr || a->grad == nullptr) return (int)hipErrorInvalidValue;
-  if (a->enc == nullptr) {  // no encoding image wanted: the one-pass producer / consumer kernel
-#ifndef MLI_FF_TPW
-#define MLI_FF_TPW 8
-#endif
-    const int blocks = (tiles + MLI_FF_TPW - 1) / MLI_FF_TPW;
-    hipLaunchKernelGGL(field_fused_kernel, dim3(blocks), dim3(FF_WAVES * 64), FF_LDS, (hipStream_t)s, *a,
-                       MLI_FF_TPW);
-    MLI_LAUNCH_CHECK();
-  }
+  if (a->enc == nullptr) return (int)hipErrorInvalidValue;
   // FIELD: phase A (encodings of the 5 points) then phase B (layer 0 + softplus + sdf head),
   // in chunks of tiles (a chunk's encodings: tiles x 40 KiB).  Measured at 4096 x 128 samples
   // with the geometry prefetched beside the heads: 1024 / 2048 / 4096 / 8192 /

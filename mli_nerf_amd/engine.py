@@ -90,10 +90,6 @@ class RenderEngine:
         self.u_fine = (C.c_float * 64)(*(layout.u_fine(cfg.n_fine) + [2.0] * (64 - cfg.n_fine)))
         self._pack_descs = None
         self.trace = None  # set to a list to record per-round sampler outputs (debug/tests)
-        # FIELD without an encoding image (mli_sdf with enc = NULL: the one-pass producer /
-        # consumer kernel) wherever nothing re-reads the encodings, i.e. everywhere but stage-a
-        # training; False forces the two-phase kernels (A/B, tests)
-        self.field_one_pass = False
         # fixed-order reductions instead of fp32 atomics in mli_wgrad / mli_hash_bwd:
         # bit-reproducible gradients at the cost of partial-slab traffic
         self.deterministic = False
@@ -206,10 +202,10 @@ class RenderEngine:
         out["_keep"] = (w2c, w2l, K, ridx)
         return out
 
-    def _sdf(self, rays, dists, n_per_ray, out, mode=0, grad=None, hess=None, h0=None, need_enc=True):
+    def _sdf(self, rays, dists, n_per_ray, out, mode=0, grad=None, hess=None, h0=None):
         R = rays["center"].shape[0]
         enc = None
-        if mode == 1 and (need_enc or not self.field_one_pass):
+        if mode == 1:
             # the FIELD encoding image (stage a's backward re-reads it)
             tiles = (R * n_per_ray + 31) // 32
             enc = self._buf("enc5", (tiles * 32 * 640,), torch.float16)
@@ -264,8 +260,7 @@ class RenderEngine:
         grad = self._buf("grad", (N, R, 3))
         hess = self._buf("hess", (N, R, 3)) if training else None
         h0 = self._buf("h0", (S * 256,), torch.float16)
-        enc = self._sdf(rays, dists, N, sdf, mode=1, grad=grad, hess=hess, h0=h0,
-                        need_enc=training and self.stage == "a")
+        enc = self._sdf(rays, dists, N, sdf, mode=1, grad=grad, hess=hess, h0=h0)
         return dict(sdf=sdf, grad=grad, hess=hess, h0=h0, enc=enc)
 
     def pq_mode(self, N, training):

@@ -254,7 +254,6 @@ class Model(torch.nn.Module):
         self.image_width = self.image_size_train[1]
         self.deterministic = False  # fixed-order gradient reductions (RenderEngine.deterministic)
         self.pq = True              # stage-b output-layer dW from the forward's partials (RenderEngine.pq)
-        self.field_one_pass = False  # FIELD without the encoding image (measured slower in the step)
 
     # -------------------------------------------------------------- parameter plumbing
     def _view(self, name, flat=None):
@@ -377,7 +376,6 @@ class Model(torch.nn.Module):
         eng = self.engine
         eng.deterministic = self.deterministic
         eng.pq = self.pq
-        eng.field_one_pass = self.field_one_pass
         eng.set_normal_eps(sdf.normal_eps)
         eng.active_levels = int(sdf.active_levels)
         l0 = sdf.mlp.linears[0]

@@ -7,13 +7,7 @@ rounded to fp16 up to one fp16 ulp (|e| <= 2^-10 |v| + 2^-24; the oracle sums th
 another order).  At the finest levels most taps leave the center's cell (the job path); the
 coarse levels reuse the center's corners -- both are covered, and the stage-a case masks the
 levels >= active_levels (coarse-to-fine) to zero.  The FIELD outputs built on this image (sdf,
-normals, hessian, h0) are checked against the oracle in tests/test_gpu_parity.py.
-
-Stage b and inference run FIELD in one pass (``field_fused_kernel``: no encoding image, the
-gathers and layer 0 as producer / consumer waves through LDS).  It is checked here against the
-two-phase path on the same samples: h0 bit-identical (same encodings, same MFMA chains), sdf /
-normal / hessian equal up to the regrouped sdf-head sum."""
-from margins import check
+normals, hessian, h0) are checked against the oracle in tests/test_gpu_parity.py."""
 import pytest
 import torch
 
@@ -42,7 +36,6 @@ def test_encoding_image_matches_oracle(config, R, Nc, Nf, H, active):
     model.prepare()
     eng = model.engine
     eng.active_levels = active
-    eng.field_one_pass = False  # the two-phase path writes the encoding image under test
     data = {k: v.to(DEV) for k, v in synthetic.make_batch(R, H=cfg.data.train.image_size[0],
                                                           W=cfg.data.train.image_size[1], frame=3).items()}
     rays = eng.rays(data["pose"], data["intr"], data["pose_light"], data["ray_idx"], cfg.data.train.image_size[1])
@@ -74,47 +67,3 @@ def test_encoding_image_matches_oracle(config, R, Nc, Nf, H, active):
     bad = err > tol
     assert not bad.any(), (int(bad.sum()), float(err.max()))
 
-
-@pytest.mark.parametrize("config,R,Nc,Nf,H,training", [("syn_hotdog_b", 512, 32, 16, 2, True),
-                                                        ("syn_hotdog_b", 100, 16, 5, 1, False),   # ragged tile
-                                                        ("syn_hotdog_b", 256, 64, 16, 4, True)])
-def test_one_pass_field_matches_two_phase(config, R, Nc, Nf, H, training):
-    if not torch.cuda.is_available():
-        pytest.skip("no HIP device")
-    from mli_nerf_amd.model import Model
-    log2T = 19
-    cfg = preset(config, rays=R, n_coarse=Nc, n_fine=Nf, n_hier=H, log2T=log2T)
-    model = Model(cfg.model, cfg.data)
-    model.load_state_dict(synthetic.make_state_dict(log2T=log2T, heads="rgb_r_s"))
-    model = model.to(DEV)
-    model.train(training)
-    model.prepare()
-    eng = model.engine
-    data = {k: v.to(DEV) for k, v in synthetic.make_batch(R, H=cfg.data.train.image_size[0],
-                                                          W=cfg.data.train.image_size[1], frame=5).items()}
-    rays = eng.rays(data["pose"], data["intr"], data["pose_light"], data["ray_idx"], cfg.data.train.image_size[1])
-    dists = eng.sample(rays)
-    outs = []
-    for one_pass in (False, True):
-        eng.field_one_pass = one_pass
-        fld = eng.field(rays, dists, training)
-        assert (fld["enc"] is None) == one_pass
-        outs.append({k: (None if v is None else v.clone()) for k, v in fld.items() if k != "enc"})
-    torch.cuda.synchronize()
-    two, one = outs
-    S = dists.numel()
-    assert torch.equal(one["h0"][:S * 256], two["h0"][:S * 256])
-    sdf_err = (one["sdf"] - two["sdf"]).abs().max().item()
-    check("one-pass sdf max abs vs two-phase", sdf_err, 1e-5)
-    # grad = tap sdf differences / (4 eps): the regrouped sdf-head sum moves each tap by a few
-    # ulps, so measure |grad diff| in tap-sdf ulps / (4 eps) ((|s| + 1) 2^-23 / grad_den)
-    gunit = (two["sdf"].abs() + 1.0) * 2.0 ** -23 / eng.grad_den
-    gu = ((one["grad"] - two["grad"]).norm(dim=-1) / gunit).reshape(-1)
-    check("one-pass grad p99 |diff| in sdf ulps / (4 eps)", torch.quantile(gu, 0.99).item(), 16.0)
-    check("one-pass grad max |diff| in sdf ulps / (4 eps)", gu.max().item(), 128.0)
-    if training:
-        # hess = (sum of taps / 2 - 2 s0) / eps^2: in units of sdf ulps (|s| + 1) * 2^-23 / eps^2
-        unit = (two["sdf"].abs()[..., None] + 1.0) * 2.0 ** -23 / eng.hess_den
-        hu = ((one["hess"] - two["hess"]).abs() / unit).reshape(-1)
-        check("one-pass hessian p99 |diff| in sdf ulps / eps^2", torch.quantile(hu, 0.99).item(), 16.0)
-        check("one-pass hessian max |diff| in sdf ulps / eps^2", hu.max().item(), 128.0)

@@ -62,11 +62,7 @@ def main():
     R, N = args.rays, model.pcfg.n_samples
     res = {}
     res["sample (all rounds)"] = timeit(lambda: eng.sample(rays, None), args.reps)
-    eng.field_one_pass = False
     res["sdf field"] = timeit(lambda: eng.field(rays, dists, True), args.reps)
-    eng.field_one_pass = True
-    res["sdf field one-pass"] = timeit(lambda: eng.field(rays, dists, True), args.reps)
-    eng.field_one_pass = False
     res["heads fwd train"] = timeit(lambda: eng.heads(rays, dists, fld, True), args.reps)
     res["heads fwd eval"] = timeit(lambda: eng.heads(rays, dists, fld, False), args.reps)
     hd = eng.heads(rays, dists, fld, True)
@@ -78,7 +74,6 @@ def main():
     res["backward (all)"] = timeit(lambda: eng.backward(st, d, d, d1, d, model.flat, model._sdf_l1(), g), args.reps)
     res["pack heads"] = timeit(lambda: eng.pack_heads(model.flat.detach(), model._sdf_l1()), args.reps)
     flops = {"sdf field": kernel_flops("mli_sdf:field", R, N, 64, 16, 4),
-             "sdf field one-pass": kernel_flops("mli_sdf:field", R, N, 64, 16, 4),
              "heads fwd train": kernel_flops("mli_rgb_fwd", R, N, 64, 16, 4),
              "heads fwd eval": kernel_flops("mli_rgb_fwd", R, N, 64, 16, 4)}
     for k, (med, mn) in res.items():

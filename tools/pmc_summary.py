@@ -28,7 +28,7 @@ def short(name):
              ("dw4_partial_kernel", "mli_dw4"), ("dw4_reduce_kernel", "mli_dw4:reduce"),
              ("wgrad_kernel<256, 256", "mli_wgrad:big"), ("wgrad_dma_kernel<256, 256", "mli_wgrad:big"), ("wgrad_kernel<256, 320", "mli_wgrad:wide"),
              ("wgrad_kernel<32, 256", "mli_wgrad:thin"), ("wgrad_dma_kernel<256, 320", "mli_wgrad:wide"), ("encode5_kernel", "mli_sdf:field/encode5"),
-             ("field_mlp_kernel", "mli_sdf:field/mlp"), ("field_fused_kernel", "mli_sdf:field/fused"), ("sdf_kernel", "mli_sdf:sdf"), ("sample_fine_kernel", "mli_sample_fine"),
+             ("field_mlp_kernel", "mli_sdf:field/mlp"), ("sdf_kernel", "mli_sdf:sdf"), ("sample_fine_kernel", "mli_sample_fine"),
              ("composite_fwd_kernel", "mli_composite_fwd"), ("composite_bwd_kernel", "mli_composite_bwd"),
              ("composite_loss_kernel", "mli_composite_loss"), ("composite_loss_finalize", "mli_composite_loss:finalize"),
              ("adamw_kernel", "mli_adamw"), ("pack_kernel", "mli_pack")]
