@@ -711,6 +711,9 @@ def main(argv=None):
         "roofline": roof, "kernels": ktab,
         "mfma_tflops_step": round(sum(kernel_flops(n, R, N, 64, args.fine, 4, model.stage) for n in ktab) /
                                   (step_ms * 1e-3) / 1e12, 2),
+        # peak HBM held by torch's allocator: the prefetch lanes each hold a full set of step buffers
+        "hbm_peak_gib": (round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)
+                         if torch.device(dev).type == "cuda" else None),
     }
     if rehearse:  # every rank shared ONE GPU over gloo: a process-flow check, not a scaling number
         result["config"]["rehearsal"] = "%d ranks on one GPU, gloo collectives" % world

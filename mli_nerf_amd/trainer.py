@@ -335,7 +335,13 @@ class Trainer:
     @prefetch_depth.setter
     def prefetch_depth(self, d):
         """The lanes rotate modulo depth + 1: a change while prefetched batches are pending could
-        point the next prefetch at a lane still in use, so it is refused then."""
+        point the next prefetch at a lane still in use, so it is refused then.
+
+        Memory: the prefetch runs the whole step inside its lane's buffer set, so each lane holds a
+        full set of per-step buffers (activations xT / x0T / feat, dZ, masks, the encoding image,
+        the dW slabs): about 7.5 GiB per lane at 4096 x 128 samples and about 22 GiB at the
+        reference's 8192 x 192 -- depth 2 (three lanes) is affordable on the 288 GB of an MI355X,
+        and bench.py reports the allocator's peak as ``hbm_peak_gib``."""
         d = int(d)
         if d < 1:
             raise ValueError("prefetch_depth must be >= 1")
