@@ -29,6 +29,9 @@
  *   frag image: fp16 activations of a 32-sample tile in MFMA B-operand register order,
  *   [S/32][ksteps][64 lanes][8 halves] (16 B per lane per k-step, 1 KiB per wave load).
  *   feature-major: [features][S] fp16 rows (S contiguous), in tile order m.
+ *   tile-blocked (ABI 14): [S/256][features][256] fp16 -- the 256 samples of one workgroup
+ *   of every feature row contiguous; the training activation / gradient images the weight
+ *   gradients read (x0T, xT, dzT, dz1T) use it.
  *
  * Reference interface each entry point replaces is cited per function
  * (paths relative to the liulisixin/MLI-NeRF checkout).
@@ -44,7 +47,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mli_stream_t; /* == hipStream_t */
 
-#define MLI_ABI_VERSION 13
+#define MLI_ABI_VERSION 14
 #define MLI_HIDDEN 256
 #define MLI_LEVELS 16
 #define MLI_LEVEL_FEAT 8
@@ -175,8 +178,8 @@ typedef struct {
   float* y;               /* [N][R][8] rgb(3) o_r(3) o_s(1) pad                            */
   uint16_t* feat_frag;    /* scratch frag image [S/32][16][64][8]                          */
   /* training outputs (NULL in inference) */
-  uint16_t* x0T;          /* [MLI_HEAD_K0][S] feature-major head input                      */
-  uint16_t* xT;           /* [3 heads][4 layers][256][S] feature-major X1..X4               */
+  uint16_t* x0T;          /* [S/256][MLI_HEAD_K0][256] tile-blocked head input (ABI 14)     */
+  uint16_t* xT;           /* [3 heads][4 layers] x [S/256][256][256] tile-blocked X1..X4    */
   uint32_t* masks;        /* [3][4][S/32][64][4] ReLU bit masks of X1..X4                   */
   int n_heads;            /* 3: LumenRGB 'rgb_r_s' (stage b); 1: mode 'rgb' (stage a, head mlp) */
   /* Output-layer partials (training, N % 32 == 0; both NULL: off).  The composite weights do not
@@ -241,7 +244,8 @@ typedef struct {
   const float* dz4;       /* [N][R][8] */
   const void* wbwd;       /* packed transposed weight chunks (mli_pack)                     */
   const uint32_t* masks;  /* from mli_rgb_fwd */
-  uint16_t* dzT;          /* [3 heads][4 layers][256][S] feature-major dZ0..dZ3 (scaled)    */
+  uint16_t* dzT;          /* [3 heads][4 layers] x [S/256][256][256] tile-blocked dZ0..dZ3
+                             (scaled)                                                        */
   uint16_t* dz4T;         /* [3 heads][4][S] feature-major dZ4 rows (scaled), or NULL (PQ mode:
                              the output-layer dW comes from mli_dw4)                          */
 } mli_rgb_bwd_args;
@@ -260,12 +264,15 @@ int mli_rgb_bwd_workspace(const mli_rgb_bwd_args* a, int64_t* bytes);
  * this call launches (bit mask), so a caller can time them separately.  Split-K is sized
  * per class to fill the 256 CUs. */
 typedef struct {
-  const uint16_t* a_rows; /* dZ^T rows [M][S] */
-  const uint16_t* b_rows; /* X^T  rows [K][S] */
+  const uint16_t* a_rows; /* dZ^T rows [M][S] (a_tiled: [S/256][M][256]) */
+  const uint16_t* b_rows; /* X^T  rows [K][S] (b_tiled: [S/256][K][256]) */
   int M, K;               /* logical rows of A and B */
   float* dw;              /* [M][ldw] fp32; this job writes columns [0, K) */
   float* db;              /* [M] fp32 or NULL */
   int ldw;                /* row stride of dw (>= K) */
+  int a_tiled, b_tiled;   /* 1: the operand is a tile-blocked image (S % 256 == 0): sample m of
+                             row r at (m / 256) * rows * 256 + r * 256 + m % 256, the layout
+                             mli_rgb_fwd / mli_rgb_bwd / mli_geo_bwd write (ABI 14)         */
 } mli_wgrad_job;
 #define MLI_WGRAD_BIG 1
 #define MLI_WGRAD_WIDE 2
@@ -344,10 +351,10 @@ typedef struct {
                              W1sdf^T of the stage-a layout (mli_nerf_amd/layout.py geo_plan) */
   const uint32_t* masks;  /* head 0 masks from mli_rgb_fwd */
   const uint16_t* feat_frag; /* feat frag image from mli_rgb_fwd */
-  uint16_t* dzT;          /* [4 layers][256][S] */
+  uint16_t* dzT;          /* [4 layers] x [S/256][256][256] tile-blocked */
   uint16_t* dz4T;         /* [4][S] */
   float* d_nrm;           /* [N][R][4] scaled d total / d normal (xyz, pad) */
-  uint16_t* dz1T;         /* [256][S] feature-major dZ1sdf (scaled) */
+  uint16_t* dz1T;         /* [S/256][256][256] tile-blocked dZ1sdf (scaled) */
   uint16_t* dh0_frag;     /* [S/32][16][64][8] d h0 (scaled, layer-1 path only) */
 } mli_geo_bwd_args;
 int mli_geo_bwd(const mli_geo_bwd_args* a, mli_stream_t s);

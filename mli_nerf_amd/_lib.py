@@ -73,7 +73,8 @@ class RgbBwdArgs(C.Structure):
 
 
 class WgradJob(C.Structure):
-    _fields_ = [("a_rows", P), ("b_rows", P), ("M", I32), ("K", I32), ("dw", P), ("db", P), ("ldw", I32)]
+    _fields_ = [("a_rows", P), ("b_rows", P), ("M", I32), ("K", I32), ("dw", P), ("db", P), ("ldw", I32),
+                ("a_tiled", I32), ("b_tiled", I32)]
 
 
 class WgradArgs(C.Structure):
@@ -187,7 +188,7 @@ class FragRowsArgs(C.Structure):
                 ("ld", I64), ("col0", I64), ("row0", I32)]
 
 
-ABI_VERSION = 13  # include/mli_hip.h MLI_ABI_VERSION
+ABI_VERSION = 14  # include/mli_hip.h MLI_ABI_VERSION
 
 ENTRY_POINTS = {
     "mli_rays": RaysArgs, "mli_hashgrid_fwd": HashgridArgs, "mli_sdf": SdfArgs,

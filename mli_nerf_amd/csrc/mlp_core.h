@@ -137,6 +137,15 @@ MLI_FI void ring_start(Ring& r, const void* base, int n, Bytes&& bytes) {
 }
 
 // ---------------------------------------------------------------------- LDS staging
+// The training activation / gradient images the weight gradients read (x0T, xT, dzT; stage a:
+// dzT, dz1T) are tile-blocked: [S/256][rows][256] fp16 per matrix, so one workgroup's 256 samples
+// of every row are one contiguous rows x 512 B block (a staged 32-row tile: 16 KiB contiguous),
+// and mli_wgrad's 64-sample stages read 128 B segments 512 B apart instead of S * 2 bytes apart
+// (tools/read_pattern_bench.hip: 6.3 against 5.6 TB/s in the BIG shape).  Element (row, m) of a
+// matrix with `rows` rows sits at tiled_off(m, rows) + row * TROW.
+constexpr int TROW = 256;
+MLI_FI size_t tiled_off(size_t m, int rows) { return (m >> 8) * (size_t)rows * TROW + (m & 255); }
+
 // stage_tile() writes a feature-major tile (accumulator layout: rows acc_row(i, h), sample
 // column wave*32 + c) into one buffer; the next phase's barrier makes it visible and
 // stage_flush() writes it out (16 B per lane, NW * 64 B per row) while the other buffer takes
@@ -165,15 +174,17 @@ MLI_FI void stage_tile(Stager& sg, uint8_t* lds, half8 f0, half8 f1, uint16_t* d
 }
 
 template <class G, int ROLE>
-MLI_FI void stage_flush(Stager& sg, const uint8_t* lds, int S) {
+MLI_FI void stage_flush(Stager& sg, const uint8_t* lds, int) {
   // ALL: every thread; STORE: the second half of the waves; DMA: none
+  static_assert(G::SAMPLES == TROW, "one 256-sample block per workgroup");
   constexpr int NS = G::template flush_ops<ROLE>();
   constexpr int RSTEP = G::template flushers<ROLE>() / G::TPR;
   const int t = ROLE == STORE ? threadIdx.x - G::THREADS / 2 : threadIdx.x;
   const int row = t / G::TPR, col = t % G::TPR;
   const uint8_t* sb = lds + G::STAGE_OFF + sg.pbuf * G::STAGE + row * G::SROW + col * 16;
-  uint16_t* g = sg.pend + (size_t)row * S + col * 8;
-  const size_t step = (size_t)RSTEP * S;
+  // tile-blocked image: the staged 32 rows of this workgroup's block are 32 x 512 B contiguous
+  uint16_t* g = sg.pend + (size_t)row * TROW + col * 8;
+  const size_t step = (size_t)RSTEP * TROW;
 #pragma unroll
   for (int u = 0; u < NS; ++u) {
     const u32x4 x = *reinterpret_cast<const u32x4*>(sb + RSTEP * u * G::SROW);
@@ -520,9 +531,10 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
       B[18][j] = (f16)v18;
       if (TRAIN) {
         // feature-major rows 256..303 (k_nat order) from the fp32 sources
-        a.x0T[(size_t)k_nat(16, h, j) * S + m] = __builtin_bit_cast(uint16_t, (f16)v16);
-        a.x0T[(size_t)k_nat(17, h, j) * S + m] = __builtin_bit_cast(uint16_t, (f16)v17);
-        a.x0T[(size_t)k_nat(18, h, j) * S + m] = __builtin_bit_cast(uint16_t, (f16)v18);
+        uint16_t* x0m = a.x0T + tiled_off(m, MLI_HEAD_K0);
+        x0m[k_nat(16, h, j) * TROW] = __builtin_bit_cast(uint16_t, (f16)v16);
+        x0m[k_nat(17, h, j) * TROW] = __builtin_bit_cast(uint16_t, (f16)v17);
+        x0m[k_nat(18, h, j) * TROW] = __builtin_bit_cast(uint16_t, (f16)v18);
       }
     }
   }
@@ -557,7 +569,7 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
       fl[0] = A[2 * t];
       fl[64] = A[2 * t + 1];
     }
-    if (TRAIN) stage_tile<G>(sg, lds, A[2 * t], A[2 * t + 1], a.x0T + (size_t)(32 * t) * S + col0, lane);
+    if (TRAIN) stage_tile<G>(sg, lds, A[2 * t], A[2 * t + 1], a.x0T + col0 * MLI_HEAD_K0 + (32 * t) * TROW, lane);
   };
   run_layer_d<G, ROLE, 16, 8, 2, 0, 0, HEADS_DEFER>(rg, lds, sg, S, B, lane, bytes, NoPre{}, none, feat_epi, pacc);
   if (HEADS_DEFER) {
@@ -592,7 +604,7 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
           if (t & 1) mbits[t >> 1] |= bits << 16; else mbits[t >> 1] = bits;
           if (stg)
             stage_tile<G>(sg, lds, out[2 * t], out[2 * t + 1],
-                          a.xT + ((size_t)(hd * XL + layer) * 256 + 32 * t) * S + col0, lane);
+                          a.xT + (size_t)(hd * XL + layer) * 256 * S + col0 * 256 + (32 * t) * TROW, lane);
           if (t == 7) {
             u32x4* mp = reinterpret_cast<u32x4*>(a.masks) +
                         ((size_t)(hd * 4 + layer) * (S / 32) + tile) * 64 + lane;
@@ -744,7 +756,7 @@ MLI_FI void rgb_bwd_body(const mli_rgb_bwd_args& a, uint8_t* lds) {
         out[2 * t] = acc_to_frag(v, 0);
         out[2 * t + 1] = acc_to_frag(v, 1);
         stage_tile<G>(sg, lds, out[2 * t], out[2 * t + 1],
-                      a.dzT + ((size_t)(hd * 4 + layer) * 256 + 32 * t) * S + col0, lane);
+                      a.dzT + (size_t)(hd * 4 + layer) * 256 * S + col0 * 256 + (32 * t) * TROW, lane);
       };
     };
     auto e3 = mask_epi(A, 3, 0);

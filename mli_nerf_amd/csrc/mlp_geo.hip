@@ -77,7 +77,7 @@ __global__ __launch_bounds__(GGeo::THREADS) void geo_bwd_kernel(mli_geo_bwd_args
       for (int i = 0; i < 16; ++i) v[i] = mask_bit(acc[i], word, (t & 1) * 16 + i);
       out[2 * t] = acc_to_frag(v, 0);
       out[2 * t + 1] = acc_to_frag(v, 1);
-      stage_tile<G>(sg, lds, out[2 * t], out[2 * t + 1], a.dzT + ((size_t)layer * 256 + 32 * t) * S + col0, lane);
+      stage_tile<G>(sg, lds, out[2 * t], out[2 * t + 1], a.dzT + (size_t)layer * 256 * S + col0 * 256 + (32 * t) * TROW, lane);
     };
   };
   run_layer<G, ALL, 1, 8, true, 0, false>(rg, lds, sg, S, &z4, lane, bytes, pre(0), mask_epi(A, 3, 0));
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(GGeo::THREADS) void geo_bwd_kernel(mli_geo_bwd_args
         }
       A[2 * t] = acc_to_frag(v, 0);
       A[2 * t + 1] = acc_to_frag(v, 1);
-      stage_tile<G>(sg, lds, A[2 * t], A[2 * t + 1], a.dz1T + (size_t)(32 * t) * S + col0, lane);
+      stage_tile<G>(sg, lds, A[2 * t], A[2 * t + 1], a.dz1T + col0 * 256 + (32 * t) * TROW, lane);
     } else {
       float* dn = a.d_nrm + 4 * slot;
       if (h == 0) {

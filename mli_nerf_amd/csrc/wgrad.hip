@@ -22,7 +22,14 @@ struct Job {
   int M, K, ldw;
   float* dw; float* db;
   int tiles_n, tile_base;
+  int a_tiled, b_tiled;  // operand layout: 0 rows [n][S], 1 tile-blocked [S/256][n][256] (mlp_core.h TROW)
 };
+
+// Address of (row, sample k .. k + 63) of an operand with n_rows rows: feature-major rows or the
+// tile-blocked image (a 64-sample stage never crosses a 256-sample block: k is a multiple of 64).
+MLI_FI const uint16_t* operand_at(const uint16_t* base, bool tiled, int n_rows, int row, size_t S, int k) {
+  return tiled ? base + (size_t)(k >> 8) * n_rows * 256 + (size_t)row * 256 + (k & 255) : base + (size_t)row * S + k;
+}
 
 struct KArgs {
   Job jobs[MAXJOBS];
@@ -34,13 +41,13 @@ struct KArgs {
 
 // Rows [t*ROWS, t*ROWS + ROWS) x BK samples from k, 8 x 16 B per row, rows clamped to n_rows.
 template <int ROWS, int LOADS, bool KEEP = false>
-MLI_FI void stage_load(u32x4 (&st)[LOADS], const uint16_t* __restrict__ base, int n_rows, int t,
+MLI_FI void stage_load(u32x4 (&st)[LOADS], const uint16_t* __restrict__ base, bool tiled, int n_rows, int t,
                        size_t S, int k, int tid) {
 #pragma unroll
   for (int u = 0; u < LOADS; ++u) {
     const int id = u * 512 + tid, row = min(id >> 3, ROWS - 1), col = id & 7;
     const int gr = min(t * ROWS + row, n_rows - 1);
-    const u32x4* src = reinterpret_cast<const u32x4*>(base + gr * S + k + col * 8);
+    const u32x4* src = reinterpret_cast<const u32x4*>(operand_at(base, tiled, n_rows, gr, S, k) + col * 8);
     // streamed once: non-temporal (leave L2 to the dW atomics); KEEP: rows other workgroups of
     // this XCD read next (a shared B operand), through L2
     st[u] = KEEP ? *src : __builtin_nontemporal_load(src);
@@ -105,8 +112,8 @@ __global__ __launch_bounds__(512) void wgrad_kernel(KArgs ka) {
   // clamped prefetch: past the slice end it reloads the last valid k-step (never consumed)
   auto load = [&](int d, int kk) MLI_LAMBDA_FI {
     const int kc = min(kk, k1 - BK);
-    stage_load<BM, A_LOADS>(sa[d], J.a, J.M, tm, S, kc, tid);
-    stage_load<BN, B_LOADS, SHARE_B>(sb[d], J.b, J.K, tn, S, kc, tid);
+    stage_load<BM, A_LOADS>(sa[d], J.a, J.a_tiled, J.M, tm, S, kc, tid);
+    stage_load<BN, B_LOADS, SHARE_B>(sb[d], J.b, J.b_tiled, J.K, tn, S, kc, tid);
   };
   auto step = [&](int d, int kk) MLI_LAMBDA_FI {
     __syncthreads();
@@ -230,21 +237,27 @@ __global__ __launch_bounds__(512) void wgrad_dma_kernel(KArgs ka) {
   // this lane's DMA source rows (piece u * 8 + wave, clamped: a duplicate of the last piece
   // rewrites the same bytes, so every wave issues PPW per stage and the vmcnt counts are uniform)
   const uint16_t* src[PPW];
-  int dst[PPW];
+  int dst[PPW], bst[PPW];  // bst: the tile-blocked operand's block stride (halves), 0: rows layout
 #pragma unroll
   for (int u = 0; u < PPW; ++u) {
     const int piece = min(u * 8 + wave, PIECES - 1);
     const int row = piece * RPI + lane / CPR, pos = lane % CPR;
     const int c = swz<BKD>(row, pos);  // the chunk that belongs at this position
-    const uint16_t* rp = row < BM ? J.a + (size_t)min(tm * BM + row, J.M - 1) * S
-                                  : J.b + (size_t)min(tn * BN + row - BM, J.K - 1) * S;
-    src[u] = rp + c * 8;
+    const bool in_a = row < BM;
+    const bool tiled = in_a ? J.a_tiled : J.b_tiled;
+    const int n_rows = in_a ? J.M : J.K;
+    const int gr = in_a ? min(tm * BM + row, J.M - 1) : min(tn * BN + row - BM, J.K - 1);
+    src[u] = operand_at(in_a ? J.a : J.b, tiled, n_rows, gr, S, 0) + c * 8;
+    bst[u] = tiled ? n_rows * 256 : 0;
     dst[u] = piece * 1024;
   }
   auto issue = [&](int s, int buf) MLI_LAMBDA_FI {
     const int kk = min(k0 + s * BKD, k1 - BKD);  // past the end: a dummy refetch, never consumed
 #pragma unroll
-    for (int u = 0; u < PPW; ++u) glds16(src[u] + kk, lds + buf * STAGE + dst[u]);
+    for (int u = 0; u < PPW; ++u) {
+      const size_t off = bst[u] ? (size_t)(kk >> 8) * bst[u] + (kk & 255) : (size_t)kk;
+      glds16(src[u] + off, lds + buf * STAGE + dst[u]);
+    }
   };
 
   f32x16 acc[TM][TN];
@@ -477,6 +490,8 @@ int64_t plan(const mli_wgrad_args* a, int cls, KArgs& ka) {
     if (n == MAXJOBS || j.ldw < j.K || j.M <= 0 || j.K <= 0) return -1;
     Job& J = ka.jobs[n++];
     J.a = j.a_rows; J.b = j.b_rows; J.M = j.M; J.K = j.K; J.ldw = j.ldw; J.dw = j.dw; J.db = j.db;
+    J.a_tiled = j.a_tiled ? 1 : 0; J.b_tiled = j.b_tiled ? 1 : 0;
+    if ((J.a_tiled || J.b_tiled) && a->S % 256 != 0) return -1;
     J.tiles_n = (j.K + BN - 1) / BN;
     tiles += ((j.M + BM - 1) / BM) * J.tiles_n;
   }

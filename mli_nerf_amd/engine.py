@@ -469,14 +469,15 @@ class RenderEngine:
                 db = dwbuf[off + m * k:off + m * k + m]
                 off += m * k + m
                 if li == 0:
-                    jobs.append(L.WgradJob(L.ptr(dzT[hdx, 0]), L.ptr(hd["x0T"]), m, k, L.ptr(dw), L.ptr(db), k))
+                    jobs.append(L.WgradJob(L.ptr(dzT[hdx, 0]), L.ptr(hd["x0T"]), m, k, L.ptr(dw), L.ptr(db), k, 1, 1))
                 elif li < 4:
                     jobs.append(L.WgradJob(L.ptr(dzT[hdx, li]), L.ptr(hd["xT"][hdx, li - 1]), m, k, L.ptr(dw),
-                                           L.ptr(db), k))
+                                           L.ptr(db), k, 1, 1))
                 elif pq:
                     dw4[hdx], db4[hdx], k4[hdx] = L.ptr(dw), L.ptr(db), m
                 else:
-                    jobs.append(L.WgradJob(L.ptr(dz4T[hdx]), L.ptr(hd["xT"][hdx, 3]), m, k, L.ptr(dw), L.ptr(db), k))
+                    jobs.append(L.WgradJob(L.ptr(dz4T[hdx]), L.ptr(hd["xT"][hdx, 3]), m, k, L.ptr(dw), L.ptr(db), k,
+                                           0, 1))
                 pre = layout.param_prefix(name, li)
                 v = self.param_view(flat, pre + ".weight_v")
                 g = self.param_view(flat, pre + ".weight_g")
@@ -573,7 +574,8 @@ class RenderEngine:
             w, b = take(m, k)
             a_rows = bufs["dzT"][li] if li < 4 else bufs["dz4T"]
             b_rows = bufs["x0T"] if li == 0 else bufs["xT"][0, li - 1]
-            jobs_s.append(L.WgradJob(L.ptr(a_rows), L.ptr(b_rows), m, k, L.ptr(w), L.ptr(b), k))
+            # dZ0..dZ3 and X: tile-blocked images; dZ4 rows are feature-major
+            jobs_s.append(L.WgradJob(L.ptr(a_rows), L.ptr(b_rows), m, k, L.ptr(w), L.ptr(b), k, 1 if li < 4 else 0, 1))
             pre = layout.param_prefix(head, li)
             k_ref = pv(pre + ".weight_v").shape[1]
             kinv = layout.head_kinv(head, k_ref) if li == 0 else np.arange(k_ref)
@@ -583,7 +585,7 @@ class RenderEngine:
             keep.append(kt)
         # neural_sdf.mlp.linears.1: dZ1sdf x h0 (S samples)
         w, b = take(256, 256)
-        jobs_s.append(L.WgradJob(L.ptr(bufs["dz1T"]), L.ptr(bufs["h0_rows"]), 256, 256, L.ptr(w), L.ptr(b), 256))
+        jobs_s.append(L.WgradJob(L.ptr(bufs["dz1T"]), L.ptr(bufs["h0_rows"]), 256, 256, L.ptr(w), L.ptr(b), 256, 1, 0))
         pre = "neural_sdf.mlp.linears.1"
         d, kt = self._assemble_desc(w, b, pv(pre + ".weight_v"), pv(pre + ".weight_g"), 256, 256, 256,
                                     np.arange(256), gv(pre + ".weight_v"), gv(pre + ".weight_g"), gv(pre + ".bias"))

@@ -165,3 +165,11 @@ def q4_segs(N):
     if 256 % N == 0:
         return 256 // N
     return 1 if N % 256 == 0 else 256 // N + 2
+
+
+def untile(img, rows):
+    """A tile-blocked activation image ([S/256][rows][256], include/mli_hip.h ABI 14) as
+    feature-major rows [rows][S] (a view copy, for inspection and tests)."""
+    flat = img.reshape(-1)
+    S = flat.numel() // rows
+    return flat.view(S // 256, rows, 256).permute(1, 0, 2).reshape(rows, S)

@@ -22,7 +22,8 @@ pts = c_g[..., None, :] + v_g[..., None, :] * d_g
 sd16 = fp16_table_sd(sd)
 _, feat = o_render.sdf_net(sd16, pcfg, pts, with_feat=True)      # [1,R,N,256]
 feat_t = feat[0].reshape(S, 256).t()                              # [256, S] tile order m = r*N+k
-x0T = hd["x0T"].float().cpu()
+from mli_nerf_amd import layout  # noqa: E402
+x0T = layout.untile(hd["x0T"], 304).float().cpu()  # tile-blocked image -> [304][S]
 e = (x0T[:256] - feat_t).abs()
 print("x0T feat rows: max err %.3e (max |feat| %.3e)" % (e.max(), feat_t.abs().max()))
 p = pts[0].reshape(S, 3).t()
@@ -38,10 +39,10 @@ print("x0T light err %.3e view err %.3e" % ((x0T[272:288] - light).abs().max(), 
 xin = torch.cat([pts, o_render.sh16(v_g[..., None, :].expand_as(pts)), F.normalize(g.reshape(1, R, N, 3), dim=-1), feat,
                  o_render.sh16(rays["pts_light"].cpu()[None, :, None, :].expand_as(pts))], -1)[0].reshape(S, -1)
 h = xin
-for li in range(4):
+for li in range(hd["xT"].shape[1]):
     pre = "neural_rgb.mlp.linears.%d" % li
     h = F.relu(F.linear(h, o_render.wn(sd, pre), sd[pre + ".bias"]))
-    xg = hd["xT"][0, li].float().cpu()
+    xg = layout.untile(hd["xT"][0, li], 256).float().cpu()
     print("head0 X%d err %.3e (max %.3e)" % (li + 1, (xg - h.t()).abs().max(), h.abs().max()))
 torch.set_printoptions(precision=4, linewidth=200, sci_mode=False)
 print("gpu x0T rows 256..263, samples 0..5:\n", x0T[256:264, :6])
