@@ -163,3 +163,15 @@ def test_source_hash_detects_stale_library(tmp_path, monkeypatch):
     monkeypatch.setattr(B, "REPO", "/elsewhere/repo")
     monkeypatch.setattr(B, "FLAGS", [f.replace(ROOT, "/elsewhere/repo") for f in B.FLAGS])
     assert B.source_hash() == want
+
+
+def test_untile_inverts_the_tile_blocked_layout():
+    """layout.untile (the host's view of the ABI 14 tile-blocked images) against the index rule
+    include/mli_hip.h states: sample m of row r at (m / 256) * rows * 256 + r * 256 + m % 256."""
+    import torch
+    from mli_nerf_amd import layout
+    rows, S = 5, 768
+    out = layout.untile(torch.arange(rows * S, dtype=torch.int64), rows)
+    assert out.shape == (rows, S)
+    for r, m in ((0, 0), (3, 517), (4, 767), (1, 255), (2, 256)):
+        assert out[r, m].item() == (m // 256) * rows * 256 + r * 256 + m % 256
