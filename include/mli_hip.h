@@ -28,10 +28,14 @@
  *   workgroups of 256 (8 waves).  S must be a multiple of 32.
  *   frag image: fp16 activations of a 32-sample tile in MFMA B-operand register order,
  *   [S/32][ksteps][64 lanes][8 halves] (16 B per lane per k-step, 1 KiB per wave load).
+ *   Element j of lane l = c + 32 h of k-step q is sample c of the tile and feature
+ *     NAT order: 16 q + 8 h + j                        (the hash-grid encodings)
+ *     ACC order: 16 q + 8 (j >> 2) + 4 h + (j & 3)    (an MFMA accumulator tile's registers:
+ *                h0, feat, and every training activation / gradient image the weight
+ *                gradients read -- x0 (= feat_frag), xT, dzT, dz4T, dz1T; ABI 15)
  *   feature-major: [features][S] fp16 rows (S contiguous), in tile order m.
  *   tile-blocked (ABI 14): [S/256][features][256] fp16 -- the 256 samples of one workgroup
- *   of every feature row contiguous; the training activation / gradient images the weight
- *   gradients read (x0T, xT, dzT, dz1T) use it.
+ *   of every feature row contiguous (still accepted by mli_wgrad).
  *
  * Reference interface each entry point replaces is cited per function
  * (paths relative to the liulisixin/MLI-NeRF checkout).
@@ -47,7 +51,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mli_stream_t; /* == hipStream_t */
 
-#define MLI_ABI_VERSION 14
+#define MLI_ABI_VERSION 15
 #define MLI_HIDDEN 256
 #define MLI_LEVELS 16
 #define MLI_LEVEL_FEAT 8
@@ -176,10 +180,12 @@ typedef struct {
   const uint16_t* h0;     /* frag image from mli_sdf FIELD                                 */
   const void* wfwd;       /* packed forward weight chunks (mli_pack)                       */
   float* y;               /* [N][R][8] rgb(3) o_r(3) o_s(1) pad                            */
-  uint16_t* feat_frag;    /* scratch frag image [S/32][16][64][8]                          */
+  uint16_t* feat_frag;    /* the heads' layer-0 input image x0, [S/32][MLI_HEAD_K0/16][64][8] ACC
+                             order: k-steps 0..15 the SDF feature (SDF layer 1's output, the
+                             heads re-read it), in training also k-steps 16..18 (p, normal,
+                             pad, SH(light), SH(view)) -- the WIDE dW operand (ABI 15)         */
   /* training outputs (NULL in inference) */
-  uint16_t* x0T;          /* [S/256][MLI_HEAD_K0][256] tile-blocked head input (ABI 14)     */
-  uint16_t* xT;           /* [3 heads][4 layers] x [S/256][256][256] tile-blocked X1..X4    */
+  uint16_t* xT;           /* [3 heads][4 layers] x [S/32][16][64][8] ACC frag images X1..X4 */
   uint32_t* masks;        /* [3][4][S/32][64][4] ReLU bit masks of X1..X4                   */
   int n_heads;            /* 3: LumenRGB 'rgb_r_s' (stage b); 1: mode 'rgb' (stage a, head mlp) */
   /* Output-layer partials (training, N % 32 == 0; both NULL: off).  The composite weights do not
@@ -197,7 +203,7 @@ typedef struct {
 /* ray segments per 256-sample workgroup (an upper bound; N % 32 == 0) */
 #define MLI_Q4_SEGS(N) ((256 % (N)) == 0 ? 256 / (N) : ((N) % 256 == 0 ? 1 : 256 / (N) + 2))
 int mli_rgb_fwd(const mli_rgb_fwd_args* a, mli_stream_t s);
-/* bytes[0..5]: y, feat_frag, x0T, xT, masks, q4 (x0T, xT, masks 0 unless `train` = xT != NULL is
+/* bytes[0..5]: y, feat_frag, 0, xT, masks, q4 (xT, masks 0 unless `train` = xT != NULL is
  * requested by setting a->xT to any non-NULL value before the query; q4 0 unless a->weights is
  * non-NULL, which also drops X3 from xT). */
 int mli_rgb_fwd_workspace(const mli_rgb_fwd_args* a, int64_t* bytes);
@@ -244,10 +250,10 @@ typedef struct {
   const float* dz4;       /* [N][R][8] */
   const void* wbwd;       /* packed transposed weight chunks (mli_pack)                     */
   const uint32_t* masks;  /* from mli_rgb_fwd */
-  uint16_t* dzT;          /* [3 heads][4 layers] x [S/256][256][256] tile-blocked dZ0..dZ3
+  uint16_t* dzT;          /* [3 heads][4 layers] x [S/32][16][64][8] ACC frag images dZ0..dZ3
                              (scaled)                                                        */
-  uint16_t* dz4T;         /* [3 heads][4][S] feature-major dZ4 rows (scaled), or NULL (PQ mode:
-                             the output-layer dW comes from mli_dw4)                          */
+  uint16_t* dz4T;         /* [3 heads] x [S/32][1][64][8] frag images of dZ4 (rows 0..2, scaled),
+                             or NULL (PQ mode: the output-layer dW comes from mli_dw4)         */
 } mli_rgb_bwd_args;
 int mli_rgb_bwd(const mli_rgb_bwd_args* a, mli_stream_t s);
 /* bytes[0..1]: dzT, dz4T. */
@@ -264,16 +270,24 @@ int mli_rgb_bwd_workspace(const mli_rgb_bwd_args* a, int64_t* bytes);
  * this call launches (bit mask), so a caller can time them separately.  Split-K is sized
  * per class to fill the 256 CUs. */
 typedef struct {
-  const uint16_t* a_rows; /* dZ^T rows [M][S] (a_tiled: [S/256][M][256]) */
-  const uint16_t* b_rows; /* X^T  rows [K][S] (b_tiled: [S/256][K][256]) */
+  const uint16_t* a_rows; /* dZ^T [M rows][S samples] in layout a_tiled */
+  const uint16_t* b_rows; /* X^T  [K rows][S samples] in layout b_tiled */
   int M, K;               /* logical rows of A and B */
   float* dw;              /* [M][ldw] fp32; this job writes columns [0, K) */
   float* db;              /* [M] fp32 or NULL */
   int ldw;                /* row stride of dw (>= K) */
-  int a_tiled, b_tiled;   /* 1: the operand is a tile-blocked image (S % 256 == 0): sample m of
-                             row r at (m / 256) * rows * 256 + r * 256 + m % 256, the layout
-                             mli_rgb_fwd / mli_rgb_bwd / mli_geo_bwd write (ABI 14)         */
+  int a_tiled, b_tiled;   /* operand layout (MLI_WGRAD_LAYOUT_*): 0 feature-major rows [rows][S];
+                             1 tile-blocked (S % 256 == 0): sample m of row r at
+                             (m / 256) * rows * 256 + r * 256 + m % 256; 2 / 3 frag image in ACC /
+                             NAT order (S % 64 == 0): the tile of sample m at (m / 32) * kst
+                             k-steps -- the layout mli_rgb_fwd / mli_rgb_bwd / mli_geo_bwd write
+                             (ABI 15).  A job's two operands are both frag images or neither.    */
+  int a_kst, b_kst;       /* frag images: k-steps per 32-sample tile (>= ceil(rows / 16)); else 0 */
 } mli_wgrad_job;
+#define MLI_WGRAD_LAYOUT_ROWS 0
+#define MLI_WGRAD_LAYOUT_TILED 1
+#define MLI_WGRAD_LAYOUT_FRAG_ACC 2
+#define MLI_WGRAD_LAYOUT_FRAG_NAT 3
 #define MLI_WGRAD_BIG 1
 #define MLI_WGRAD_WIDE 2
 #define MLI_WGRAD_THIN 4
@@ -341,8 +355,8 @@ int mli_composite_bwd_geo(const mli_composite_bwd_geo_args* a, mli_stream_t s);
 int mli_composite_bwd_geo_workspace(const mli_composite_bwd_geo_args* a, int64_t* bytes);
 
 /* dX chain of the single head down to its inputs, then through SDF layer 1:
- * dZ3..dZ0 (feature-major, for the head dW), dX0 -> d feat (frag order) and d normal,
- * dZ1sdf = d feat * softplus'(z1) (feature-major, for dW of neural_sdf.mlp.linears.1) and
+ * dZ3..dZ0 (ACC frag images, for the head dW), dX0 -> d feat (frag order) and d normal,
+ * dZ1sdf = d feat * softplus'(z1) (ACC frag image, for dW of neural_sdf.mlp.linears.1) and
  * d h0 of the center point = W1^T dZ1sdf (frag image, ACC order as the h0 image). */
 typedef struct {
   int R, N;
@@ -350,11 +364,11 @@ typedef struct {
   const void* wgeo;       /* packed chunks (mli_pack): W4^T, W3^T, W2^T, W1^T, W0^T (9 n-tiles),
                              W1sdf^T of the stage-a layout (mli_nerf_amd/layout.py geo_plan) */
   const uint32_t* masks;  /* head 0 masks from mli_rgb_fwd */
-  const uint16_t* feat_frag; /* feat frag image from mli_rgb_fwd */
-  uint16_t* dzT;          /* [4 layers] x [S/256][256][256] tile-blocked */
-  uint16_t* dz4T;         /* [4][S] */
+  const uint16_t* feat_frag; /* x0 image from mli_rgb_fwd (feat = its k-steps 0..15) */
+  uint16_t* dzT;          /* [4 layers] x [S/32][16][64][8] ACC frag images dZ0..dZ3 (scaled) */
+  uint16_t* dz4T;         /* [S/32][1][64][8] frag image of dZ4 (rows 0..2, scaled) */
   float* d_nrm;           /* [N][R][4] scaled d total / d normal (xyz, pad) */
-  uint16_t* dz1T;         /* [S/256][256][256] tile-blocked dZ1sdf (scaled) */
+  uint16_t* dz1T;         /* [S/32][16][64][8] ACC frag image dZ1sdf (scaled) */
   uint16_t* dh0_frag;     /* [S/32][16][64][8] d h0 (scaled, layer-1 path only) */
 } mli_geo_bwd_args;
 int mli_geo_bwd(const mli_geo_bwd_args* a, mli_stream_t s);

@@ -51,7 +51,7 @@ class SampleFineArgs(C.Structure):
 class RgbFwdArgs(C.Structure):
     _fields_ = [("R", I32), ("N", I32), ("center", P), ("ray_unit", P), ("pts_light", P),
                 ("dists", P), ("grad", P), ("h0", P), ("wfwd", P), ("y", P), ("feat_frag", P),
-                ("x0T", P), ("xT", P), ("masks", P), ("n_heads", I32), ("weights", P), ("q4", P)]
+                ("xT", P), ("masks", P), ("n_heads", I32), ("weights", P), ("q4", P)]
 
 
 class CompositeArgs(C.Structure):
@@ -74,7 +74,16 @@ class RgbBwdArgs(C.Structure):
 
 class WgradJob(C.Structure):
     _fields_ = [("a_rows", P), ("b_rows", P), ("M", I32), ("K", I32), ("dw", P), ("db", P), ("ldw", I32),
-                ("a_tiled", I32), ("b_tiled", I32)]
+                ("a_tiled", I32), ("b_tiled", I32), ("a_kst", I32), ("b_kst", I32)]
+
+
+# mli_wgrad_job operand layouts (MLI_WGRAD_LAYOUT_*)
+ROWS, TILED, FRAG_ACC, FRAG_NAT = 0, 1, 2, 3
+
+
+def frag_job(a, b, M, K, dw, db, ldw, a_kst, b_kst, order=FRAG_ACC):
+    """A mli_wgrad job over two fragment images (ABI 15) with a_kst / b_kst k-steps per tile."""
+    return WgradJob(a, b, M, K, dw, db, ldw, order, order, a_kst, b_kst)
 
 
 class WgradArgs(C.Structure):
@@ -188,7 +197,7 @@ class FragRowsArgs(C.Structure):
                 ("ld", I64), ("col0", I64), ("row0", I32)]
 
 
-ABI_VERSION = 14  # include/mli_hip.h MLI_ABI_VERSION
+ABI_VERSION = 15  # include/mli_hip.h MLI_ABI_VERSION
 
 ENTRY_POINTS = {
     "mli_rays": RaysArgs, "mli_hashgrid_fwd": HashgridArgs, "mli_sdf": SdfArgs,
@@ -237,13 +246,19 @@ def lib():
         if _lib.mli_abi_version() != ABI_VERSION:
             raise ImportError("libmli_hip.so ABI mismatch")
         from . import build as _build
-        # in-tree sources: the library must match them (an experiment build named by MLI_HIP_LIB is
-        # built from a modified tree on purpose and is not checked)
-        if all(os.path.exists(d) for d in _build._deps()) and not os.environ.get("MLI_HIP_LIB"):
+        # in-tree sources: the in-tree library must match them.  Only a library OUTSIDE the in-tree
+        # build output (an experiment build named by MLI_HIP_LIB, built from a modified tree on
+        # purpose) is exempt, and it is reported when its sources differ from the tree's.
+        if all(os.path.exists(d) for d in _build._deps()):
             want, got = _build.source_hash(), _lib.mli_source_hash().decode()
-            if got != want:
+            in_tree = os.path.realpath(LIB_PATH) == os.path.realpath(_build.OUT)
+            if got != want and in_tree:
                 raise ImportError("libmli_hip.so is stale (built from sources %s, the tree is %s); rebuild with "
                                   "mli_nerf_amd.build.build()" % (got, want))
+            if got != want:
+                import warnings
+                warnings.warn("MLI_HIP_LIB=%s was built from sources %s, not this tree's %s (experiment build)"
+                              % (LIB_PATH, got, want))
     return _lib
 
 

@@ -24,7 +24,7 @@ extern "C" int mli_rgb_bwd_workspace(const mli_rgb_bwd_args* a, int64_t* bytes) 
   const int64_t S = (int64_t)a->R * a->N;
   if (S <= 0 || S % 256 != 0) return (int)hipErrorInvalidValue;
   bytes[0] = 3 * 4 * 256 * S * 2;  // dzT
-  bytes[1] = 3 * 4 * S * 2;        // dz4T
+  bytes[1] = 3 * S * 16 * 2;       // dz4T (one-k-step fragment images)
   return 0;
 }
 

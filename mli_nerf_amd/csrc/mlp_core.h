@@ -17,9 +17,9 @@
 //    stores issued since stay in flight: vmcnt counts loads and stores in issue order)
 //    and a raw s_barrier (no __syncthreads fence, which would drain the stores);
 //  * epilogues are fused: softplus(beta=100) for the SDF feature layer, ReLU (+ bit masks
-//    + feature-major activation stores for the weight gradients in training), sigmoid
-//    for the outputs.  Feature-major tiles are transposed through LDS so each 256-sample
-//    row leaves as 512 contiguous bytes.
+//    + the activation stores for the weight gradients in training), sigmoid for the outputs.
+//    The training activation / gradient images are fragment images (ABI 15, below): every wave
+//    stores its own registers, 1 KiB contiguous per k-step, no LDS transpose.
 #pragma once
 #include "common.h"
 
@@ -28,24 +28,27 @@
 namespace {
 
 constexpr int CH(int ks) { return ks * 1024 + 128; }
-constexpr int FRAG_TILE = 16 * 64 * 8;  // halves per 32-sample tile of a 256-wide frag image
+constexpr int FRAG_KS = 512;            // halves per k-step of a 32-sample tile's frag image (1 KiB)
+constexpr int FRAG_TILE = 16 * FRAG_KS;  // halves per 32-sample tile of a 256-wide frag image
+// the head layer-0 input image x0 (feat k-steps 0..15 + the extras 16..18) per 32-sample tile
+constexpr int X0_KS = MLI_HEAD_K0 / 16;
+constexpr int X0_TILE = X0_KS * FRAG_KS;
+constexpr int Q4_SLOT = 257 * 16;  // one wave's output-layer partials Q in LDS (PQ mode, q4_tile)
 constexpr int DIST = 2;                 // chunks in flight ahead of the one being read (3: no gain)
 constexpr int NSLOT = DIST + 1;
 
-// Wave roles.  ALL: every wave issues its share of the weight DMAs and of the activation
-// flushes, and waits.  Split queues (DMA + STORE): vmcnt retires vector-memory ops in issue
-// order, so a wave that both streams weights and stores activations waits, for every weight
-// chunk, on the activation stores it issued before that chunk's DMAs.  The first half of the
-// waves (DMA) issue all the LDS-DMA (weights, ReLU masks) and are the only waves that wait on
-// vmcnt in the phase loop; the second half (STORE) issue all the activation flushes and never
-// wait on them.
+// Wave roles.  ALL: every wave issues its share of the weight DMAs and waits.  Split (DMA +
+// STORE): the first half of the waves (DMA) issue all the LDS-DMA (weights, ReLU masks) and are
+// the only waves that wait on vmcnt in the phase loop; the second half (STORE) never wait there.
+// Every wave stores its own activation fragments; vmcnt retires vector-memory ops in issue
+// order, so the DMA waves' counted waits include the stores they issued after the chunk waited
+// for (static counts per phase).
 enum Role { ALL = 0, DMA = 1, STORE = 2 };
 
 // Workgroup geometry: NW waves of 32 samples (NW * 32 samples per workgroup), a weight ring of
 // NSLOT slots for chunks of up to MAXP 1 KiB pieces, split (DMA + STORE) or ALL wave roles.
-// The ring DMA of one chunk is ND waves x RND pieces of 1 KiB (16 B per lane); the
-// feature-major staging tile is [32 features][NW * 32 samples] fp16, double buffered; the
-// backward's ReLU-mask blocks are NW tiles x 1 KiB, double buffered.
+// The ring DMA of one chunk is ND waves x RND pieces of 1 KiB (16 B per lane); the backward's
+// ReLU-mask blocks are NW tiles x 1 KiB, double buffered.
 template <int NW_, int MAXP, bool SPLIT_, int PF_ = 0>
 struct Geo {
   static constexpr int NW = NW_;
@@ -56,16 +59,17 @@ struct Geo {
   static constexpr int ND = SPLIT ? NW / 2 : NW;
   static constexpr int RND = (MAXP + ND - 1) / ND;
   static constexpr int SLOT = RND * ND * 1024;
-  static constexpr int SROW = SAMPLES * 2 + 16;  // 16 B pad
-  static constexpr int STAGE = 32 * SROW;
-  static constexpr int STAGE_OFF = NSLOT * SLOT;
+  static constexpr int RING = NSLOT * SLOT;
   static constexpr int MASKB = NW * 1024;
-  static constexpr int MASK_OFF = STAGE_OFF + 2 * STAGE;
-  static constexpr int LDS_FWD = STAGE_OFF + 2 * STAGE;
+  static constexpr int MASK_OFF = RING;
+  static constexpr int LDS_FWD = RING;
   static constexpr int LDS_BWD = MASK_OFF + 2 * MASKB;
-  // per-wave transpose scratch of the output-layer partials (rgb_fwd PQ mode, q4_tile)
+  // PQ mode (rgb_fwd, q4_tile): the waves' Q partials parked for the cross-wave sum, then the
+  // per-wave transpose scratch
+  static constexpr int QP_OFF = RING;
   static constexpr int PQ_WAVE = 2048 + 256;
-  static constexpr int LDS_FWD_PQ = LDS_FWD + NW * PQ_WAVE;
+  static constexpr int PQW_OFF = QP_OFF + NW * Q4_SLOT;
+  static constexpr int LDS_FWD_PQ = PQW_OFF + NW * PQ_WAVE;
   // PQ mode: the first FEAT_KS k-steps of each wave's feat fragments also stay in a wave-private
   // LDS block, so the three heads re-read only the rest from the frag image
   static constexpr int FEAT_KS = 6;
@@ -73,11 +77,8 @@ struct Geo {
   // the eval forward (no PQ blocks): 8 k-steps fit
   static constexpr int FEAT_KS_EVAL = 8;
   static constexpr int LDS_FWD_F = LDS_FWD + NW * FEAT_KS_EVAL * 1024;
-  static constexpr int TPR = SAMPLES / 8;  // 16 B flush pieces per staged row
-  // ring DMAs per wave and chunk, flush stores per wave and staged tile
+  // ring DMAs per wave and chunk
   template <int ROLE> static constexpr int ring_ops() { return ROLE == STORE ? 0 : RND; }
-  template <int ROLE> static constexpr int flushers() { return ROLE == STORE ? THREADS / 2 : THREADS; }
-  template <int ROLE> static constexpr int flush_ops() { return ROLE == DMA ? 0 : 32 * TPR / flushers<ROLE>(); }
 };
 
 // ---------------------------------------------------------------------- weight ring
@@ -136,63 +137,23 @@ MLI_FI void ring_start(Ring& r, const void* base, int n, Bytes&& bytes) {
   r.cur = 0;
 }
 
-// ---------------------------------------------------------------------- LDS staging
-// The training activation / gradient images the weight gradients read (x0T, xT, dzT; stage a:
-// dzT, dz1T) are tile-blocked: [S/256][rows][256] fp16 per matrix, so one workgroup's 256 samples
-// of every row are one contiguous rows x 512 B block (a staged 32-row tile: 16 KiB contiguous),
-// and mli_wgrad's 64-sample stages read 128 B segments 512 B apart instead of S * 2 bytes apart
-// (tools/read_pattern_bench.hip: 6.3 against 5.6 TB/s in the BIG shape).  Element (row, m) of a
-// matrix with `rows` rows sits at tiled_off(m, rows) + row * TROW.
-constexpr int TROW = 256;
-MLI_FI size_t tiled_off(size_t m, int rows) { return (m >> 8) * (size_t)rows * TROW + (m & 255); }
-
-// stage_tile() writes a feature-major tile (accumulator layout: rows acc_row(i, h), sample
-// column wave*32 + c) into one buffer; the next phase's barrier makes it visible and
-// stage_flush() writes it out (16 B per lane, NW * 64 B per row) while the other buffer takes
-// the next tile.
-struct Stager {
-  uint16_t* pend;  // global address of (row 0, first sample of the block) of the staged tile
-  int buf, pbuf;
-};
-
-template <class G>
-MLI_FI void stage_tile(Stager& sg, uint8_t* lds, half8 f0, half8 f1, uint16_t* dst, int lane) {
-  // f0 / f1 = acc_to_frag(v, 0 / 1): element i of the tile is half (i & 1) of word (i & 7) >> 1
-  // of fragment i >> 3; it goes to row acc_row(i, h), column wave*32 + c
-  const int wave = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
-  uint8_t* sb = lds + G::STAGE_OFF + sg.buf * G::STAGE + (4 * h) * G::SROW + (wave * 32 + c) * 2;
-  const u32x4 w[2] = {__builtin_bit_cast(u32x4, f0), __builtin_bit_cast(u32x4, f1)};
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const uint32_t word = w[i >> 3][(i & 7) >> 1];
-    *reinterpret_cast<uint16_t*>(sb + ((i & 3) + 8 * (i >> 2)) * G::SROW) =
-        (uint16_t)((i & 1) ? (word >> 16) : word);
-  }
-  sg.pend = dst;
-  sg.pbuf = sg.buf;
-  sg.buf ^= 1;
-}
-
-template <class G, int ROLE>
-MLI_FI void stage_flush(Stager& sg, const uint8_t* lds, int) {
-  // ALL: every thread; STORE: the second half of the waves; DMA: none
-  static_assert(G::SAMPLES == TROW, "one 256-sample block per workgroup");
-  constexpr int NS = G::template flush_ops<ROLE>();
-  constexpr int RSTEP = G::template flushers<ROLE>() / G::TPR;
-  const int t = ROLE == STORE ? threadIdx.x - G::THREADS / 2 : threadIdx.x;
-  const int row = t / G::TPR, col = t % G::TPR;
-  const uint8_t* sb = lds + G::STAGE_OFF + sg.pbuf * G::STAGE + row * G::SROW + col * 16;
-  // tile-blocked image: the staged 32 rows of this workgroup's block are 32 x 512 B contiguous
-  uint16_t* g = sg.pend + (size_t)row * TROW + col * 8;
-  const size_t step = (size_t)RSTEP * TROW;
-#pragma unroll
-  for (int u = 0; u < NS; ++u) {
-    const u32x4 x = *reinterpret_cast<const u32x4*>(sb + RSTEP * u * G::SROW);
-    // streaming (non-temporal) store: the activations are re-read only by a later kernel, so
-    // they should not evict the weight chunks every phase re-reads from L2
-    __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(g + u * step));
-  }
-  sg.pend = nullptr;
+// ---------------------------------------------------------------------- activation images
+// The training activation / gradient images the weight gradients read (the head input x0, X1..X3,
+// dZ0..dZ3; stage a: dZ0..dZ4, dZ1sdf) are fragment images (ABI 15): [S/32][k-steps][64 lanes]
+// [8 halves] fp16 in ACC order -- element j of lane (c, h) of k-step q is feature
+// 16 q + 8 (j >> 2) + 4 h + (j & 3) of sample c of the 32-sample tile, exactly the registers
+// acc_to_frag() produces.  Each wave stores its own fragments, 16 B per lane, 1 KiB contiguous
+// per k-step (a tile's k-steps contiguous); mli_wgrad reads them back through LDS with
+// transposing reads (ds_read_b64_tr_b16).  Measured against the tile-blocked rows of ABI 14
+// (16 ds_write_b16 per lane into an LDS transpose tile, then 16 B flushes by the STORE waves):
+// rgb_bwd 0.86 -> 0.74 ms, rgb_fwd 1.09 -> 1.05 ms, step 4.07 -> 3.85 ms (profiles/r5/direct).
+MLI_FI void frag_store2(uint16_t* tile_img, int t, half8 f0, half8 f1, int lane) {
+  // k-steps 2t and 2t+1 of the tile (a 32-feature accumulator tile t)
+  half8* d = reinterpret_cast<half8*>(tile_img) + (2 * t) * 64 + lane;
+  // streaming (non-temporal) stores: the activations are re-read only by a later kernel, so
+  // they should not evict the weight chunks every phase re-reads from L2
+  __builtin_nontemporal_store(f0, d);
+  __builtin_nontemporal_store(f1, d + 64);
 }
 
 // ReLU as one v_max_i32 on the bit pattern: fmaxf on an MFMA result adds a canonicalising
@@ -267,30 +228,17 @@ MLI_FI f32x16 chunk_mma(const uint8_t* chunk, const half8* X, int lane) {
 }
 
 // One layer of NT n-tiles over KS k-steps; epi(t, acc) consumes each finished tile.
-// Static store counts (for the counted vmcnt): STAGED = the layer stages its tiles (the
-// flush of tile t-1 at t >= 1; the flush at t == 0 is decided at run time and not counted),
-// EPI = unconditional global stores per epilogue, MASKED = one mask store at t == NT-1;
-// pre.issue(t) issues pre.count(t) VMEM ops ahead of the weight DMAs.  STORE waves never
-// wait in the loop: nothing they issue lands in LDS.
-template <class G, int ROLE, int KS, int NT, bool STAGED, int EPI, bool MASKED, class Bytes, class Pre, class Epi>
-MLI_FI void run_layer(Ring& rg, uint8_t* lds, Stager& sg, int S, const half8* X, int lane, Bytes&& bytes,
-                      Pre&& pre, Epi&& epi) {
-  constexpr int FL = ROLE == ALL ? G::template flush_ops<ALL>() : 0;  // flush stores in this wave's queue
-  // VMEM ops a phase issues after its weight DMAs (flush + epilogue stores), per t in the layer
-  auto stores = [](int t) MLI_LAMBDA_FI {
-    return ((t > 0 && STAGED) ? FL : 0) + EPI + ((MASKED && t == NT - 1) ? 1 : 0);
-  };
+// Static store counts (for the counted vmcnt): EPI = unconditional global stores per epilogue,
+// MASKED = one mask store at t == NT-1; pre.issue(t) issues pre.count(t) VMEM ops ahead of the
+// weight DMAs.  STORE waves never wait in the loop: nothing they issue lands in LDS.
+template <class G, int ROLE, int KS, int NT, int EPI, bool MASKED, class Bytes, class Pre, class Epi>
+MLI_FI void run_layer(Ring& rg, uint8_t* lds, const half8* X, int lane, Bytes&& bytes, Pre&& pre, Epi&& epi) {
+  // VMEM ops a phase issues after its weight DMAs (epilogue stores), per t in the layer
+  auto stores = [](int t) MLI_LAMBDA_FI { return EPI + ((MASKED && t == NT - 1) ? 1 : 0); };
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     pre.issue(t);
     ring_issue<G, ROLE>(rg, lds, bytes);
-    if (ROLE != DMA) {
-      if (t == 0) {
-        if (sg.pend) stage_flush<G, ROLE>(sg, lds, S);
-      } else if (STAGED) {
-        stage_flush<G, ROLE>(sg, lds, S);
-      }
-    }
     const f32x16 acc = chunk_mma<KS, G::PF>(lds + (rg.cur % NSLOT) * G::SLOT, X, lane);
     epi(t, acc);
     // retire chunk cur+1 (its DMAs went out DIST-1 phases ago): every VMEM op issued after
@@ -318,21 +266,21 @@ struct NoPre {
 
 // run_layer with the epilogue deferred by one tile (DEFER): phase t issues the MFMA chain of tile
 // t, then epi(t - 1) on the accumulators carried across the barrier (pacc), so the wave's own
-// epilogue VALU / LDS work has the chain's MFMAs to hide behind instead of following them.  The
-// last tile's epilogue is the caller's: the next layer runs it as `prev` at its first phase,
-// before its chain in program order (it produces that chain's last k-steps).  Flushes follow the
-// stager at run time (a tile staged in phase t leaves in phase t + 1); the static store counts of
-// the vmcnt waits count only what is known to be issued after the chunk being retired (EPI
-// stores of epi(t - 1)); undercounting only waits longer.
+// epilogue VALU work has the chain's MFMAs to hide behind instead of following them.  The last
+// tile's epilogue is the caller's: the next layer runs it as `prev` at its first phase, before
+// its chain in program order (it produces that chain's last k-steps).  The static store counts
+// of the vmcnt waits count what is known to be issued after the chunk being retired (EPI stores
+// of epi(t - 1)); undercounting only waits longer.
 // MASKN: stores of the last tile's epilogue beyond EPI (the ReLU mask image); PREVN: stores that
-// prev issues (the previous layer's deferred last tile: its mask store).
-template <class G, int ROLE, int KS, int NT, int EPI, int MASKN, int PREVN, bool DEFER, class Bytes, class Pre,
-          class Prev, class Epi>
-MLI_FI void run_layer_d(Ring& rg, uint8_t* lds, Stager& sg, int S, const half8* X, int lane, Bytes&& bytes,
-                        Pre&& pre, Prev&& prev, Epi&& epi, f32x16& pacc) {
-  static_assert(ROLE != ALL, "split wave roles only (the flushes are not counted)");
+// prev issues (the previous layer's deferred last tile); LASTN: stores the previous layer's last
+// phase issued after its weight DMAs (retired at t = 0 with the chunk they follow).
+template <class G, int ROLE, int KS, int NT, int EPI, int MASKN, int PREVN, bool DEFER, int LASTN = 0, class Bytes,
+          class Pre, class Prev, class Epi>
+MLI_FI void run_layer_d(Ring& rg, uint8_t* lds, const half8* X, int lane, Bytes&& bytes, Pre&& pre, Prev&& prev,
+                        Epi&& epi, f32x16& pacc) {
+  static_assert(ROLE != ALL, "split wave roles only");
   auto stores = [](int t) MLI_LAMBDA_FI {
-    if (t < 0) return 0;
+    if (t < 0) return LASTN;
     const int pv = t == 0 ? PREVN : 0;
     if (DEFER) return pv + (t >= 1 ? EPI : 0);
     return pv + EPI + (t == NT - 1 ? MASKN : 0);
@@ -341,7 +289,6 @@ MLI_FI void run_layer_d(Ring& rg, uint8_t* lds, Stager& sg, int S, const half8* 
   for (int t = 0; t < NT; ++t) {
     pre.issue(t);
     ring_issue<G, ROLE>(rg, lds, bytes);
-    if (ROLE != DMA && sg.pend) stage_flush<G, ROLE>(sg, lds, S);
     if (t == 0) prev(pacc);
     const f32x16 acc = chunk_mma<KS, G::PF>(lds + (rg.cur % NSLOT) * G::SLOT, X, lane);
     if (DEFER) {
@@ -377,21 +324,19 @@ constexpr bool HEADS_DEFER = true;
 // transposed reads), ds_read_b64_tr_b16 returns them as B fragments with samples along k, and
 // two MFMAs contract them with G^T [c][samples] (rows 0..2 = g of the head's outputs, scaled by
 // MLI_Q4_SCALE into fp16 range; rows >= 3 zero).  Lane (f, h = 0) then holds Q[c = 0..3][f].
-// Each wave parks its Q (257 rows of f32x4, the last one sum_s g_sc) in the free staging area;
+// Each wave parks its Q (257 rows of f32x4, the last one sum_s g_sc) in the Q park (QP_OFF);
 // after a barrier the STORE waves sum the waves of each ray segment of the workgroup in wave
 // order (fixed order: bit-reproducible) and write q4[wg][seg] -- N = 128: two rays per workgroup,
-// a quarter of the per-tile partials -- and a second barrier frees the staging area again.
+// a quarter of the per-tile partials -- and a second barrier frees the park again.
 constexpr float Q4_SCALE = MLI_Q4_SCALE;  // g <= 1/4 -> fp16 <= 16384 (undone through mli_dw4 scale)
-constexpr int Q4_SLOT = 257 * 16;          // one wave's Q in LDS
 
 template <class G, int ROLE>
 MLI_FI void q4_tile(const mli_rgb_fwd_args& a, uint8_t* lds, const half8 (&X)[19], const float (&gq)[3], int hd,
                     int lane) {
-  static_assert(G::NW * Q4_SLOT <= 2 * G::STAGE, "Q slots in the staging area");
   const int wave = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
-  uint8_t* xr = lds + G::LDS_FWD + wave * G::PQ_WAVE;
+  uint8_t* xr = lds + G::PQW_OFF + wave * G::PQ_WAVE;
   uint8_t* gr = xr + 2048;
-  uint8_t* qs = lds + G::STAGE_OFF + wave * Q4_SLOT;
+  uint8_t* qs = lds + G::QP_OFF + wave * Q4_SLOT;
   // G^T rows 0..3 (row 3 zero) from the lanes that hold the outputs
   if (h == 0) {
 #pragma unroll
@@ -464,11 +409,11 @@ MLI_FI void q4_tile(const mli_rgb_fwd_args& a, uint8_t* lds, const half8 (&X)[19
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int w = 0; w < G::NW; ++w)
-        if ((t0 + w) * 32 / N - r_first == seg) v += *reinterpret_cast<const f32x4*>(lds + G::STAGE_OFF + w * Q4_SLOT + row * 16);
+        if ((t0 + w) * 32 / N - r_first == seg) v += *reinterpret_cast<const f32x4*>(lds + G::QP_OFF + w * Q4_SLOT + row * 16);
       __builtin_nontemporal_store(v, qo + ((size_t)seg * a.n_heads + hd) * 257 + row);
     }
   }
-  block_sync();  // the staging area is free again
+  block_sync();  // the Q park is free again
 }
 
 // ---------------------------------------------------------------------- forward
@@ -502,7 +447,9 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) B[q] = src[q * 64];
   }
-  // extras (NAT order): k-step 16 = [p, n, 0...], 17 = SH(light), 18 = SH(view)
+  // extras (NAT order): k-step 16 = [p, n, 0...], 17 = SH(light), 18 = SH(view); in training
+  // also as k-steps 16..18 of the x0 image, in ACC order (xe, stored after the prologue DMAs)
+  half8 xe[3];
   {
     const float d = a.dists[slot];
     const float* cr = a.center + 3 * r;
@@ -530,25 +477,30 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
       B[17][j] = (f16)v17;
       B[18][j] = (f16)v18;
       if (TRAIN) {
-        // feature-major rows 256..303 (k_nat order) from the fp32 sources
-        uint16_t* x0m = a.x0T + tiled_off(m, MLI_HEAD_K0);
-        x0m[k_nat(16, h, j) * TROW] = __builtin_bit_cast(uint16_t, (f16)v16);
-        x0m[k_nat(17, h, j) * TROW] = __builtin_bit_cast(uint16_t, (f16)v17);
-        x0m[k_nat(18, h, j) * TROW] = __builtin_bit_cast(uint16_t, (f16)v18);
+        // ACC element j of lane half h is row 8 (j >> 2) + 4 h + (j & 3) of the k-step:
+        // rows j / 4 + j (j < 4) and 4 + j / 8 + j (j >= 4) for h = 0 / 1
+        const int lo = j < 4 ? j : 4 + j, hi = j < 4 ? 4 + j : 8 + j;
+        xe[0][j] = (f16)sel_mask(hm, hi < 8 ? e16[hi & 7] : 0.f, lo < 8 ? e16[lo & 7] : 0.f);
+        xe[1][j] = (f16)sel_mask(hm, shl[hi], shl[lo]);
+        xe[2][j] = (f16)sel_mask(hm, shv[hi], shv[lo]);
       }
     }
   }
+  // SDF layer 1's output feat (k-steps 0..15 of the tile's x0 image; in training the image is
+  // also the WIDE dW operand, with the extras as k-steps 16..18)
+  uint16_t* ftile = a.feat_frag + (size_t)tile * X0_TILE;
   // prologue: chunks 0 .. DIST-1 in flight, wait for chunk 0
 #pragma unroll
   for (int d = 0; d < DIST; ++d) ring_issue<G, ROLE>(rg, lds, bytes);
-  if (ROLE != STORE) vm_wait((DIST - 1) * G::template ring_ops<ROLE>());
+  if (TRAIN) {
+    half8* xd = reinterpret_cast<half8*>(ftile + 16 * FRAG_KS) + lane;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) __builtin_nontemporal_store(xe[i], xd + i * 64);
+  }
+  if (ROLE != STORE) vm_wait((DIST - 1) * G::template ring_ops<ROLE>() + (TRAIN ? 3 : 0));
   block_sync();
 
-  Stager sg{nullptr, 0, 0};
-  const size_t col0 = (size_t)blockIdx.x * G::SAMPLES;
-
-  // SDF layer 1: feat = softplus(W1 h0 + b1) -> A; frag image scratch (+ x0T rows 0..255)
-  uint16_t* ftile = a.feat_frag + (size_t)tile * FRAG_TILE;
+  // SDF layer 1: feat = softplus(W1 h0 + b1) -> A and the x0 image
   f32x16 pacc;  // (HEADS_DEFER: the accumulators of the tile whose epilogue is pending)
   auto none = [](f32x16&) MLI_LAMBDA_FI {};
   auto feat_epi = [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
@@ -569,16 +521,11 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
       fl[0] = A[2 * t];
       fl[64] = A[2 * t + 1];
     }
-    if (TRAIN) stage_tile<G>(sg, lds, A[2 * t], A[2 * t + 1], a.x0T + col0 * MLI_HEAD_K0 + (32 * t) * TROW, lane);
   };
-  run_layer_d<G, ROLE, 16, 8, 2, 0, 0, HEADS_DEFER>(rg, lds, sg, S, B, lane, bytes, NoPre{}, none, feat_epi, pacc);
-  if (HEADS_DEFER) {
-    // the last feat tile, before the heads reload feat: tile 6's staged x0T rows leave first,
-    // tile 7's are made visible for the next phase's flush
-    if (TRAIN && ROLE != DMA && sg.pend) stage_flush<G, ROLE>(sg, lds, S);
-    feat_epi(7, pacc);
-    if (TRAIN) block_sync();
-  }
+  // (LASTN: the extras stores follow chunk 1's DMAs)
+  run_layer_d<G, ROLE, 16, 8, 2, 0, 0, HEADS_DEFER, TRAIN ? 3 : 0>(rg, lds, B, lane, bytes, NoPre{}, none, feat_epi,
+                                                                   pacc);
+  if (HEADS_DEFER) feat_epi(7, pacc);  // the last feat tile, before the heads reload feat
 
   for (int hd = 0; hd < a.n_heads; ++hd) {
     const int S = opaque_s(a.R * a.N);
@@ -602,9 +549,8 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
         if (TRAIN) {
           const uint32_t bits = relu_bits16(v);
           if (t & 1) mbits[t >> 1] |= bits << 16; else mbits[t >> 1] = bits;
-          if (stg)
-            stage_tile<G>(sg, lds, out[2 * t], out[2 * t + 1],
-                          a.xT + (size_t)(hd * XL + layer) * 256 * S + col0 * 256 + (32 * t) * TROW, lane);
+          if (stg) frag_store2(a.xT + ((size_t)(hd * XL + layer) * (S / 32) + tile) * FRAG_TILE, t, out[2 * t],
+                               out[2 * t + 1], lane);
           if (t == 7) {
             u32x4* mp = reinterpret_cast<u32x4*>(a.masks) +
                         ((size_t)(hd * 4 + layer) * (S / 32) + tile) * 64 + lane;
@@ -623,15 +569,20 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
         if (HEADS_DEFER) e(7, p);
       };
     };
+    // static store counts of the counted waits: X = the activation fragments of an epilogue (2),
+    // MN / PN = the mask store of a layer's last tile, in place / deferred to the next layer
     constexpr int MN = TRAIN ? 1 : 0, PN = TRAIN && HEADS_DEFER ? 1 : 0;
-    run_layer_d<G, ROLE, 19, 8, 0, MN, 0, HEADS_DEFER>(rg, lds, sg, S, B, lane, bytes, NoPre{}, none, e0, pacc);
-    run_layer_d<G, ROLE, 16, 8, 0, MN, PN, HEADS_DEFER>(rg, lds, sg, S, A, lane, bytes, NoPre{}, fin(e0), e1, pacc);
-    run_layer_d<G, ROLE, 16, 8, 0, MN, PN, HEADS_DEFER>(rg, lds, sg, S, B, lane, bytes, NoPre{}, fin(e1), e2, pacc);
-    run_layer_d<G, ROLE, 16, 8, 0, MN, PN, HEADS_DEFER>(rg, lds, sg, S, A, lane, bytes, NoPre{}, fin(e2), e3, pacc);
+    constexpr int X = TRAIN ? 2 : 0, X3 = PQ ? 0 : X;
+    constexpr int LN = HEADS_DEFER ? X : X + MN;  // stores of a layer's last phase (epi(6) when deferred)
+    run_layer_d<G, ROLE, 19, 8, X, MN, 0, HEADS_DEFER>(rg, lds, B, lane, bytes, NoPre{}, none, e0, pacc);
+    run_layer_d<G, ROLE, 16, 8, X, MN, PN + X, HEADS_DEFER, LN>(rg, lds, A, lane, bytes, NoPre{}, fin(e0), e1, pacc);
+    run_layer_d<G, ROLE, 16, 8, X, MN, PN + X, HEADS_DEFER, LN>(rg, lds, B, lane, bytes, NoPre{}, fin(e1), e2, pacc);
+    run_layer_d<G, ROLE, 16, 8, X3, MN, PN + X, HEADS_DEFER, LN>(rg, lds, A, lane, bytes, NoPre{}, fin(e2), e3, pacc);
     const int no = hd == 2 ? 1 : 3;
     const int off = hd * 3;
     float gq[3] = {0.f, 0.f, 0.f};
-    run_layer_d<G, ROLE, 16, 1, 0, 0, PN, false>(rg, lds, sg, S, B, lane, bytes, NoPre{}, fin(e3),
+    run_layer_d<G, ROLE, 16, 1, 0, 0, PN + X3, false, HEADS_DEFER ? X3 : X3 + MN>(rg, lds, B, lane, bytes, NoPre{},
+                                                                            fin(e3),
                                           [&](int, const f32x16& acc) MLI_LAMBDA_FI {
       if (h == 0) {
 #pragma unroll
@@ -646,8 +597,6 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
     // (the q4 stores come from the STORE waves only: the DMA waves' counted waits are unchanged)
     if (PQ) q4_tile<G, ROLE>(a, lds, B, gq, hd, lane);
   }
-  // (training without PQ: X3's last tile is still staged)
-  if (ROLE != DMA && sg.pend) stage_flush<G, ROLE>(sg, lds, opaque_s(a.R * a.N));
   vm_wait(0);  // no LDS-DMA may land after the workgroup's LDS is released
 }
 
@@ -712,8 +661,6 @@ MLI_FI void rgb_bwd_body(const mli_rgb_bwd_args& a, uint8_t* lds) {
   block_sync();
 
   half8 A[16], B[16];
-  Stager sg{nullptr, 0, 0};
-  const size_t col0 = (size_t)blockIdx.x * G::SAMPLES;
   for (int hd = 0; hd < 3; ++hd) {
     const int S = opaque_s(a.R * a.N);
     const int no = hd == 2 ? 1 : 3;
@@ -725,13 +672,13 @@ MLI_FI void rgb_bwd_body(const mli_rgb_bwd_args& a, uint8_t* lds) {
       if (h == 0) {
 #pragma unroll
         for (int j = 0; j < 3; ++j)
-          if (j < no) {
-            const f16 zj = (f16)dz[j];  // never bit_cast a vector element (yields element 0)
-            z4[j] = zj;
-            // the THIN dW operand (NULL: the output-layer dW comes from the forward's partials)
-            if (a.dz4T) a.dz4T[((size_t)hd * 4 + j) * S + m] = __builtin_bit_cast(uint16_t, zj);
-          }
+          if (j < no) z4[j] = (f16)dz[j];
       }
+      // the THIN dW operand, a one-k-step fragment image (rows 0..2; NULL: the output-layer dW
+      // comes from the forward's partials).  Rows j < 4 of lane half 0 are element j in both the
+      // NAT and the ACC order.
+      if (a.dz4T)
+        __builtin_nontemporal_store(z4, reinterpret_cast<half8*>(a.dz4T + ((size_t)hd * (S / 32) + tile) * FRAG_KS) + lane);
     }
     // the phase whose weight DMAs fetch the next layer's first chunk (t == 8 - DIST) issues
     // that layer's mask DMA just before them
@@ -755,8 +702,8 @@ MLI_FI void rgb_bwd_body(const mli_rgb_bwd_args& a, uint8_t* lds) {
         for (int i = 0; i < 16; ++i) v[i] = mask_bit(acc[i], word, (t & 1) * 16 + i);
         out[2 * t] = acc_to_frag(v, 0);
         out[2 * t + 1] = acc_to_frag(v, 1);
-        stage_tile<G>(sg, lds, out[2 * t], out[2 * t + 1],
-                      a.dzT + (size_t)(hd * 4 + layer) * 256 * S + col0 * 256 + (32 * t) * TROW, lane);
+        frag_store2(a.dzT + ((size_t)(hd * 4 + layer) * (S / 32) + tile) * FRAG_TILE, t, out[2 * t], out[2 * t + 1],
+                    lane);
       };
     };
     auto e3 = mask_epi(A, 3, 0);
@@ -770,20 +717,16 @@ MLI_FI void rgb_bwd_body(const mli_rgb_bwd_args& a, uint8_t* lds) {
       };
     };
     f32x16 pacc;
-    run_layer_d<G, ROLE, 1, 8, 0, 0, 0, HEADS_DEFER>(rg, lds, sg, S, &z4, lane, bytes, pre(0), none, e3, pacc);
-    run_layer_d<G, ROLE, 16, 8, 0, 0, 0, HEADS_DEFER>(rg, lds, sg, S, A, lane, bytes, pre(1), fin(e3), e2, pacc);
-    run_layer_d<G, ROLE, 16, 8, 0, 0, 0, HEADS_DEFER>(rg, lds, sg, S, B, lane, bytes, pre(2), fin(e2), e1, pacc);
-    run_layer_d<G, ROLE, 16, 8, 0, 0, 0, HEADS_DEFER>(rg, lds, sg, S, A, lane, bytes, pre(3), fin(e1), e0, pacc);
-    if (HEADS_DEFER) {
-      // the head's last tile: tile 6 (staged by the last phase) leaves first, then tile 7 is
-      // staged and made visible for the next phase's flush
-      if (ROLE != DMA && sg.pend) stage_flush<G, ROLE>(sg, lds, S);
-      e0(7, pacc);
-      block_sync();
-    }
+    // static store counts: 2 dZ fragments per epilogue (EPI, PREVN and the previous layer's last
+    // phase, LASTN)
+    constexpr int X = 2, LN = X;
+    run_layer_d<G, ROLE, 1, 8, X, 0, 0, HEADS_DEFER>(rg, lds, &z4, lane, bytes, pre(0), none, e3, pacc);
+    run_layer_d<G, ROLE, 16, 8, X, 0, X, HEADS_DEFER, LN>(rg, lds, A, lane, bytes, pre(1), fin(e3), e2, pacc);
+    run_layer_d<G, ROLE, 16, 8, X, 0, X, HEADS_DEFER, LN>(rg, lds, B, lane, bytes, pre(2), fin(e2), e1, pacc);
+    run_layer_d<G, ROLE, 16, 8, X, 0, X, HEADS_DEFER, LN>(rg, lds, A, lane, bytes, pre(3), fin(e1), e0, pacc);
+    if (HEADS_DEFER) e0(7, pacc);  // the head's last tile (its mask slot is not refilled before the
+                                   // next head's layer 0 has passed two barriers)
   }
-  // the last tile, made visible by the last phase's barrier
-  stage_flush<G, ROLE>(sg, lds, opaque_s(a.R * a.N));
   vm_wait(0);
 }
 

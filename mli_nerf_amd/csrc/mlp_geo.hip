@@ -41,8 +41,6 @@ __global__ __launch_bounds__(GGeo::THREADS) void geo_bwd_kernel(mli_geo_bwd_args
   block_sync();
 
   half8 A[16], B[16];
-  Stager sg{nullptr, 0, 0};
-  const size_t col0 = (size_t)blockIdx.x * G::SAMPLES;
   half8 z4;
   {
     const float* dz = a.dz4 + 8 * slot;
@@ -50,12 +48,10 @@ __global__ __launch_bounds__(GGeo::THREADS) void geo_bwd_kernel(mli_geo_bwd_args
     for (int j = 0; j < 8; ++j) z4[j] = (f16)0.f;
     if (h == 0) {
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const f16 zj = (f16)dz[j];
-        z4[j] = zj;
-        a.dz4T[(size_t)j * S + m] = __builtin_bit_cast(uint16_t, zj);
-      }
+      for (int j = 0; j < 3; ++j) z4[j] = (f16)dz[j];
     }
+    // the output layer's dW operand: a one-k-step fragment image (rows 0..2)
+    __builtin_nontemporal_store(z4, reinterpret_cast<half8*>(a.dz4T + (size_t)tile * FRAG_KS) + lane);
   }
   struct MaskPre {
     decltype(mask_dma)& dma;
@@ -77,16 +73,16 @@ __global__ __launch_bounds__(GGeo::THREADS) void geo_bwd_kernel(mli_geo_bwd_args
       for (int i = 0; i < 16; ++i) v[i] = mask_bit(acc[i], word, (t & 1) * 16 + i);
       out[2 * t] = acc_to_frag(v, 0);
       out[2 * t + 1] = acc_to_frag(v, 1);
-      stage_tile<G>(sg, lds, out[2 * t], out[2 * t + 1], a.dzT + (size_t)layer * 256 * S + col0 * 256 + (32 * t) * TROW, lane);
+      frag_store2(a.dzT + ((size_t)layer * tiles + tile) * FRAG_TILE, t, out[2 * t], out[2 * t + 1], lane);
     };
   };
-  run_layer<G, ALL, 1, 8, true, 0, false>(rg, lds, sg, S, &z4, lane, bytes, pre(0), mask_epi(A, 3, 0));
-  run_layer<G, ALL, 16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, pre(1), mask_epi(B, 2, 1));
-  run_layer<G, ALL, 16, 8, true, 0, false>(rg, lds, sg, S, B, lane, bytes, pre(2), mask_epi(A, 1, 2));
-  run_layer<G, ALL, 16, 8, true, 0, false>(rg, lds, sg, S, A, lane, bytes, NoPre{}, mask_epi(B, 0, 3));
+  run_layer<G, ALL, 1, 8, 2, false>(rg, lds, &z4, lane, bytes, pre(0), mask_epi(A, 3, 0));
+  run_layer<G, ALL, 16, 8, 2, false>(rg, lds, A, lane, bytes, pre(1), mask_epi(B, 2, 1));
+  run_layer<G, ALL, 16, 8, 2, false>(rg, lds, B, lane, bytes, pre(2), mask_epi(A, 1, 2));
+  run_layer<G, ALL, 16, 8, 2, false>(rg, lds, A, lane, bytes, NoPre{}, mask_epi(B, 0, 3));
   // feat frags (softplus output of SDF layer 1, forward scratch), one tile ahead of its use:
   // tile 0 now, tile t+1 ahead of phase t's weight DMAs (counted as pre-issued VMEM ops)
-  const half8* fsrc = reinterpret_cast<const half8*>(a.feat_frag + (size_t)tile * FRAG_TILE) + lane;
+  const half8* fsrc = reinterpret_cast<const half8*>(a.feat_frag + (size_t)tile * X0_TILE) + lane;
   half8 F[2][2];
   F[0][0] = fsrc[0];
   F[0][1] = fsrc[64];
@@ -104,7 +100,7 @@ __global__ __launch_bounds__(GGeo::THREADS) void geo_bwd_kernel(mli_geo_bwd_args
   // dX0 = W0^T dZ0: tiles 0..7 = d feat -> dZ1sdf = d feat * softplus'(z1), with
   // softplus'(z1) = 1 - exp(-100 feat) (torch: z/(z+1), z = e^{100 z1}; 1 past the threshold);
   // tile 8 = rows 256..287 (p 256..258, normal 259..261: (i=3,h=0), (i=0,h=1), (i=1,h=1))
-  run_layer<G, ALL, 16, 9, true, 0, false>(rg, lds, sg, S, B, lane, bytes, FeatPre{fsrc, F},
+  run_layer<G, ALL, 16, 9, 2, false>(rg, lds, B, lane, bytes, FeatPre{fsrc, F},
                                    [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
     if (t < 8) {
       f32x16 v;
@@ -117,8 +113,10 @@ __global__ __launch_bounds__(GGeo::THREADS) void geo_bwd_kernel(mli_geo_bwd_args
         }
       A[2 * t] = acc_to_frag(v, 0);
       A[2 * t + 1] = acc_to_frag(v, 1);
-      stage_tile<G>(sg, lds, A[2 * t], A[2 * t + 1], a.dz1T + col0 * 256 + (32 * t) * TROW, lane);
+      frag_store2(a.dz1T + (size_t)tile * FRAG_TILE, t, A[2 * t], A[2 * t + 1], lane);
     } else {
+      // (three store instructions, the lane halves diverging; counted as the EPI 2 of tiles 0..7:
+      // undercounting only waits longer)
       float* dn = a.d_nrm + 4 * slot;
       if (h == 0) {
         dn[0] = acc[3];
@@ -130,7 +128,7 @@ __global__ __launch_bounds__(GGeo::THREADS) void geo_bwd_kernel(mli_geo_bwd_args
   });
   // d h0 (layer-1 path) = W1sdf^T dZ1sdf -> frag image (ACC order, as the h0 image)
   uint16_t* dtile = a.dh0_frag + (size_t)tile * FRAG_TILE;
-  run_layer<G, ALL, 16, 8, false, 2, false>(rg, lds, sg, S, A, lane, bytes, NoPre{},
+  run_layer<G, ALL, 16, 8, 2, false>(rg, lds, A, lane, bytes, NoPre{},
                                     [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
     half8* dst = reinterpret_cast<half8*>(dtile) + (2 * t) * 64 + lane;
     __builtin_nontemporal_store(acc_to_frag(acc, 0), dst);
@@ -145,7 +143,7 @@ extern "C" int mli_geo_bwd_workspace(const mli_geo_bwd_args* a, int64_t* bytes) 
   const int64_t S = (int64_t)a->R * a->N;
   if (S <= 0 || S % 256 != 0) return (int)hipErrorInvalidValue;
   bytes[0] = 4 * 256 * S * 2;  // dzT
-  bytes[1] = 4 * S * 2;        // dz4T
+  bytes[1] = S * 16 * 2;       // dz4T (one-k-step fragment image)
   bytes[2] = S * 4 * 4;        // d_nrm
   bytes[3] = 256 * S * 2;      // dz1T
   bytes[4] = S * 256 * 2;      // dh0_frag

@@ -1,11 +1,14 @@
 // Weight / bias gradients of the colour heads: dW = dZ^T X, db = sum_s dZ (split-K MFMA).
 //
 // Replaces the autograd dW/db GEMMs of nn.Linear inside MLPwithSkipConnection
-// (projects/nerf/utils/nerf_util.py:186-196).  Both operands are feature-major fp16 rows
-// [rows][S] (samples contiguous), so the reduction axis (samples) is the contiguous one for
-// both MFMA operands: a plain NT GEMM.  Each workgroup owns a BM x BN output tile and a
-// k_split-sample slice; partial sums land in the fp32 outputs by atomics (few: one per
-// output element per slice), or -- deterministic mode -- go to a per-slice partial slab that
+// (projects/nerf/utils/nerf_util.py:186-196).  The operands are fp16 images of [rows][S]
+// matrices in one of three layouts (mli_wgrad_job): feature-major rows (samples contiguous, a
+// plain NT GEMM), tile-blocked rows ([S/256][rows][256]), or -- what the heads kernels write
+// since ABI 15 -- fragment images ([S/32][k-steps][64 lanes][8 halves], the accumulator
+// registers of the producing kernel), whose MFMA operands are read back through LDS with the
+// transposing ds_read_b64_tr_b16 (wgrad_frag_kernel).  Each workgroup owns a BM x BN output
+// tile and a k_split-sample slice; partial sums land in the fp32 outputs by atomics (few: one
+// per output element per slice), or -- deterministic mode -- go to a per-slice partial slab that
 // wgrad_reduce_kernel sums in slice order.
 #include "common.h"
 
@@ -22,7 +25,9 @@ struct Job {
   int M, K, ldw;
   float* dw; float* db;
   int tiles_n, tile_base;
-  int a_tiled, b_tiled;  // operand layout: 0 rows [n][S], 1 tile-blocked [S/256][n][256] (mlp_core.h TROW)
+  int a_tiled, b_tiled;  // operand layout (MLI_WGRAD_LAYOUT_*): 0 rows [n][S], 1 tile-blocked
+                         // [S/256][n][256], 2 / 3 frag image ACC / NAT order
+  int a_kst, b_kst;      // frag images: k-steps per 32-sample tile
 };
 
 // Address of (row, sample k .. k + 63) of an operand with n_rows rows: feature-major rows or the
@@ -338,6 +343,183 @@ __global__ __launch_bounds__(512) void wgrad_dma_kernel(KArgs ka) {
   }
 }
 
+// Fragment-image operands (ABI 15; wgrad_frag_kernel).  A 64-sample stage of an operand is its
+// two 32-sample tiles' k-steps, 1 KiB each and contiguous in HBM, copied by LDS-DMA one k-step per
+// wave-instruction: stage = [A: 2 tiles x KA k-steps][B: 2 tiles x KB k-steps], KA = BM / 16.
+// Within a k-step the 16 B chunk of (sample c, lane half hh) -- frag lane c + 32 hh -- lands at
+// chunk 32 hh + (c ^ (hh << 2 | (q & 1) << 3)), q the LDS k-step index: the DMA picks each lane's
+// source so.  An MFMA operand fragment (32 features x 8 samples per lane half) is two
+// ds_read_b64_tr_b16: 16-lane group g reads features 16 (g & 1) .. + 15 (k-step 2 blk + (g & 1)) of
+// 4 samples, lane 4 q' + p of the group addressing sample q' and features 4 p .. 4 p + 3, which
+// sit in frag lane half hh at byte b8 of the sample's chunk:
+//   ACC order: hh = p & 1, b8 = 8 (p >> 1);   NAT order: hh = p >> 1, b8 = 8 (p & 1).
+// A 32-lane half then reads 4 samples x 2 lane halves x 2 k-steps = 16 distinct chunk positions
+// mod 16: all 64 banks once (guide T10), conflict-free.
+MLI_FI int frag_chunk(int c, int hh, int qpar) { return 32 * hh + (c ^ ((hh << 2) | (qpar << 3))); }
+
+// byte offset inside a k-step block of lane `lane`'s transposed read r (0, 1: samples 4 r .. 4 r + 3
+// of its 8) of MFMA k-step half `half` (samples 16 half .. + 15 of the tile)
+MLI_FI int frag_read_off(int lane, int half, int r, bool nat) {
+  const int g = lane >> 4, h = lane >> 5, qq = (lane & 15) >> 2, p = lane & 3;
+  const int hh = nat ? (p >> 1) : (p & 1), b8 = nat ? 8 * (p & 1) : 8 * (p >> 1);
+  const int c = 16 * half + 8 * h + 4 * r + qq;
+  return (g & 1) * 1024 + frag_chunk(c, hh, g & 1) * 16 + b8;
+}
+
+template <int BM, int BN, int WM, int WN, int NBUF, bool SHARE_B>
+__global__ __launch_bounds__(512) void wgrad_frag_kernel(KArgs ka) {
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  constexpr int KA = BM / 16, KB = BN / 16;           // k-steps per tile of each operand's block
+  constexpr int PIECES = 2 * (KA + KB), PPW = (PIECES + 7) / 8;
+  constexpr int STAGE = PIECES * 1024, B_OFF = 2 * KA * 1024;
+  static_assert(KA % 2 == 0 && KB % 2 == 0, "operand blocks of whole 32-feature tiles");
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  int bid = blockIdx.x;
+  if (SHARE_B) {  // as wgrad_kernel
+    const int xcd = bid & 7, slot = bid >> 3;
+    const int sp = (slot / ka.n_jobs) * 8 + xcd;
+    if (sp >= ka.n_split) return;
+    bid = (slot % ka.n_jobs) * ka.n_split + sp;
+  }
+  Job J = ka.jobs[0];
+#pragma unroll
+  for (int j = 1; j < MAXJOBS; ++j)
+    if (j < ka.n_jobs && bid >= ka.jobs[j].tile_base) J = ka.jobs[j];
+  const int local = bid - J.tile_base;
+  const int split = local % ka.n_split;
+  const int tt = local / ka.n_split;
+  const int tm = tt / J.tiles_n, tn = tt - tm * J.tiles_n;
+  const int k0 = split * ka.k_split;
+  const int k1 = min(ka.S, k0 + ka.k_split);
+  if (k0 >= k1) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave - wm * WN;
+  const int h = lane >> 5, rl = lane & 31;
+
+  // this lane's DMA sources: piece u * 8 + wave (clamped: a duplicate of the last piece rewrites
+  // the same bytes, so every wave issues PPW per stage and the vmcnt counts are uniform); k-steps
+  // past the operand's last one (rows >= M or K) re-read that k-step, whose rows are discarded
+  const uint16_t* src[PPW];
+  int tstride[PPW];  // halves per 32-sample tile of the piece's image
+#pragma unroll
+  for (int u = 0; u < PPW; ++u) {
+    const int piece = min(u * 8 + wave, PIECES - 1);
+    const bool in_a = piece < 2 * KA;
+    const int pl = in_a ? piece : piece - 2 * KA, kq = in_a ? KA : KB;
+    const int tl = pl / kq, q = pl - tl * kq;
+    const int rows = in_a ? J.M : J.K, first = (in_a ? tm * BM : tn * BN) / 16;
+    const int kst = in_a ? J.a_kst : J.b_kst;
+    const int qg = min(first + q, (rows + 15) / 16 - 1);
+    const int hh = lane >> 5, c = (lane & 31) ^ ((hh << 2) | ((q & 1) << 3));
+    tstride[u] = kst * 512;
+    src[u] = (in_a ? J.a : J.b) + (size_t)tl * tstride[u] + qg * 512 + (32 * hh + c) * 8;
+  }
+  auto issue = [&](int s, int buf) MLI_LAMBDA_FI {
+    const int kk = min(k0 + s * 64, k1 - 64);  // past the end: a dummy refetch, never consumed
+#pragma unroll
+    for (int u = 0; u < PPW; ++u) {
+      const int piece = min(u * 8 + wave, PIECES - 1);
+      glds16(src[u] + (size_t)(kk >> 5) * tstride[u], lds + buf * STAGE + piece * 1024);
+    }
+  };
+  // transposed-read offsets (order per operand) for the 2 x 2 (MFMA k-step half, read) combinations
+  const bool a_nat = J.a_tiled == 3, b_nat = J.b_tiled == 3;
+  int offa[2][2], offb[2][2];
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      offa[hf][r] = frag_read_off(lane, hf, r, a_nat);
+      offb[hf][r] = B_OFF + frag_read_off(lane, hf, r, b_nat);
+    }
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  // db: the waves of output column block 0 sum their A fragments (row rl of each of their TM
+  // blocks, samples 8 h .. 8 h + 7 of every MFMA k-step), lane halves combined at the end
+  const bool do_bias = (J.db != nullptr) && tn == 0 && wn == 0;
+  float bsum[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) bsum[i] = 0.f;
+  const half2 ones = {(f16)1.f, (f16)1.f};
+
+  const int n_st = (k1 - k0) / 64;
+#pragma unroll
+  for (int d = 0; d < NBUF - 1; ++d) issue(d, d);
+  for (int st = 0; st < n_st; ++st) {
+    vm_wait((NBUF - 2) * PPW);  // this wave's DMAs of stage st have landed
+    block_sync();               // ... every wave's; and everyone is done with stage st - 1
+    issue(st + NBUF - 1, (st + NBUF - 1) % NBUF);
+    const uint8_t* sb = lds + (st % NBUF) * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int tl = ks >> 1, hf = ks & 1;
+      half8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const uint8_t* blk = sb + (tl * KA + 2 * (wm * TM + i)) * 1024;
+        const half4 lo = ds_read_tr16(blk + offa[hf][0]), hi = ds_read_tr16(blk + offa[hf][1]);
+        fa[i] = half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const uint8_t* blk = sb + (tl * KB + 2 * (wn * TN + j)) * 1024;
+        const half4 lo = ds_read_tr16(blk + offb[hf][0]), hi = ds_read_tr16(blk + offb[hf][1]);
+        fb[j] = half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(fa[i], fb[j], acc[i][j]);
+      if (do_bias) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; e += 2)
+            bsum[i] = __builtin_amdgcn_fdot2(half2{fa[i][e], fa[i][e + 1]}, ones, bsum[i], false);
+      }
+    }
+  }
+  vm_wait(0);  // the dummy refetches land before the workgroup's LDS is released
+  float* slab = nullptr;
+  if (ka.part != nullptr) {
+    int jx = 0;
+#pragma unroll
+    for (int j = 1; j < MAXJOBS; ++j)
+      if (j < ka.n_jobs && bid >= ka.jobs[j].tile_base) jx = j;
+    slab = ka.part + ka.part_base[jx] + (int64_t)split * ((int64_t)J.M * J.K + J.M);
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = tm * BM + wm * TM * 32 + i * 32 + acc_row(e, h);
+        const int col = tn * BN + wn * TN * 32 + j * 32 + rl;
+        if (row < J.M && col < J.K) {
+          if (slab) slab[(size_t)row * J.K + col] = acc[i][j][e];
+          else atomicAdd(J.dw + (size_t)row * J.ldw + col, acc[i][j][e]);
+        }
+      }
+  if (do_bias) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float v = bsum[i] + __shfl_xor(bsum[i], 32);
+      const int row = tm * BM + wm * TM * 32 + i * 32 + rl;
+      if (h == 0 && row < J.M) {
+        if (slab) slab[(size_t)J.M * J.K + row] = v;
+        else atomicAdd(J.db + row, v);
+      }
+    }
+  }
+}
+
 // Deterministic mode: out = sum over slices 0..n_split-1 (in that order) of the partial slabs.
 // One thread per output element of every job (dW [M][K] then db [M]).
 struct RArgs {
@@ -471,27 +653,43 @@ constexpr int WIDE_DMA = 2, WIDE_BKD = 64;
 // BIG through the same ring, 2 stages of 64 samples: 0.898 -> 0.847 ms (register staging of 64
 // samples before; the ring at 32-sample stages -- 64 B row segments -- measured 0.998 ms)
 constexpr int BIG_DMA = 2;
+// the fragment-image kernel (every class): 2 stages of 64 samples (BIG: 2 x 64 KiB)
+constexpr int FRAG_NBUF = 2;
 
 inline int job_class(const mli_wgrad_job& j) {
   return j.M <= 32 ? CLS_THIN : (j.K <= 256 ? CLS_BIG : CLS_WIDE);
 }
 
-// One launch per class: tiles of all its jobs x n_split k-slices, n_split sized so the
-// grid holds about OCC workgroups per CU (OCC = resident 512-thread workgroups per CU).
-// plan(): the class's jobs and split (host only; also the workspace query); returns the
-// floats of partial slabs the deterministic mode needs, -1 on invalid jobs.
+inline bool is_frag(int layout) { return layout == MLI_WGRAD_LAYOUT_FRAG_ACC || layout == MLI_WGRAD_LAYOUT_FRAG_NAT; }
+
+// a job's operands: both fragment images (with enough k-steps per tile) or neither
+inline bool job_valid(const mli_wgrad_job& j, int S) {
+  if (j.a_tiled < 0 || j.a_tiled > 3 || j.b_tiled < 0 || j.b_tiled > 3) return false;
+  const bool fa = is_frag(j.a_tiled), fb = is_frag(j.b_tiled);
+  if (fa != fb) return false;
+  if (fa && (j.a_kst < (j.M + 15) / 16 || j.b_kst < (j.K + 15) / 16)) return false;
+  if ((j.a_tiled == MLI_WGRAD_LAYOUT_TILED || j.b_tiled == MLI_WGRAD_LAYOUT_TILED) && S % 256 != 0) return false;
+  return true;
+}
+
+// One launch per class and operand kind (fragment images or rows): tiles of all its jobs x
+// n_split k-slices, n_split sized so the grid holds about OCC workgroups per CU (OCC = resident
+// 512-thread workgroups per CU).  plan(): the jobs of (cls, frag) and the split (host only; also
+// the workspace query); returns the floats of partial slabs the deterministic mode needs, -1 on
+// invalid jobs.
 template <int BM, int BN, int OCC, bool SHARE = false>
-int64_t plan(const mli_wgrad_args* a, int cls, KArgs& ka) {
+int64_t plan(const mli_wgrad_args* a, int cls, bool frag, KArgs& ka) {
   ka.S = a->S;
   int n = 0, tiles = 0;
   for (int i = 0; i < a->n_jobs; ++i) {
     const mli_wgrad_job& j = a->jobs[i];
-    if (job_class(j) != cls) continue;
+    if (!job_valid(j, a->S)) return -1;
+    if (job_class(j) != cls || is_frag(j.a_tiled) != frag) continue;
     if (n == MAXJOBS || j.ldw < j.K || j.M <= 0 || j.K <= 0) return -1;
     Job& J = ka.jobs[n++];
     J.a = j.a_rows; J.b = j.b_rows; J.M = j.M; J.K = j.K; J.ldw = j.ldw; J.dw = j.dw; J.db = j.db;
-    J.a_tiled = j.a_tiled ? 1 : 0; J.b_tiled = j.b_tiled ? 1 : 0;
-    if ((J.a_tiled || J.b_tiled) && a->S % 256 != 0) return -1;
+    J.a_tiled = j.a_tiled; J.b_tiled = j.b_tiled;
+    J.a_kst = j.a_kst; J.b_kst = j.b_kst;
     J.tiles_n = (j.K + BN - 1) / BN;
     tiles += ((j.M + BM - 1) / BM) * J.tiles_n;
   }
@@ -523,9 +721,9 @@ int64_t plan(const mli_wgrad_args* a, int cls, KArgs& ka) {
 }
 
 template <int BM, int BN, int WM, int WN, int OCC, int DEPTH, bool SHARE_B = false, int DMA_NBUF = 0, int DMA_BKD = 32>
-int launch(const mli_wgrad_args* a, int cls, hipStream_t s) {
+int launch(const mli_wgrad_args* a, int cls, bool frag, hipStream_t s) {
   KArgs ka;
-  const int64_t floats = plan<BM, BN, OCC, SHARE_B>(a, cls, ka);
+  const int64_t floats = plan<BM, BN, OCC, SHARE_B>(a, cls, frag, ka);
   if (floats < 0) return (int)hipErrorInvalidValue;
   if (ka.n_jobs == 0) return 0;
   if (a->deterministic) {
@@ -534,7 +732,15 @@ int launch(const mli_wgrad_args* a, int cls, hipStream_t s) {
   }
   int grid = 0;
   for (int i = 0; i < ka.n_jobs; ++i) grid += ((ka.jobs[i].M + BM - 1) / BM) * ka.jobs[i].tiles_n * ka.n_split;
-  if (SHARE_B && ka.share) {
+  if (frag) {
+    // fragment images: the LDS-DMA ring of 64-sample stages, FRAG_NBUF stages
+    constexpr int LDS = FRAG_NBUF * 2 * (BM / 16 + BN / 16) * 1024;
+    if (SHARE_B && ka.share)
+      hipLaunchKernelGGL((wgrad_frag_kernel<BM, BN, WM, WN, FRAG_NBUF, SHARE_B>),
+                         dim3(8 * ka.n_jobs * ((ka.n_split + 7) / 8)), dim3(512), LDS, s, ka);
+    else
+      hipLaunchKernelGGL((wgrad_frag_kernel<BM, BN, WM, WN, FRAG_NBUF, false>), dim3(grid), dim3(512), LDS, s, ka);
+  } else if (SHARE_B && ka.share) {
     grid = 8 * ka.n_jobs * ((ka.n_split + 7) / 8);
     if constexpr (SHARE_B && DMA_NBUF > 0)
       hipLaunchKernelGGL((wgrad_dma_kernel<BM, BN, WM, WN, DMA_NBUF, true, DMA_BKD>), dim3(grid), dim3(512),
@@ -570,9 +776,12 @@ int launch(const mli_wgrad_args* a, int cls, hipStream_t s) {
 extern "C" int mli_wgrad(const mli_wgrad_args* a, mli_stream_t s) {
   if (a->S <= 0 || a->S % BK != 0) return (int)hipErrorInvalidValue;
   int e = 0;
-  if (a->classes & CLS_BIG) e = launch<256, 256, 4, 2, 1, 2, false, BIG_DMA, 64>(a, CLS_BIG, (hipStream_t)s);
-  if (!e && (a->classes & CLS_WIDE)) e = launch<256, 320, 4, 2, 1, 1, WIDE_SHARE, WIDE_DMA, WIDE_BKD>(a, CLS_WIDE, (hipStream_t)s);
-  if (!e && (a->classes & CLS_THIN)) e = launch<32, 256, 1, 8, 2, 2>(a, CLS_THIN, (hipStream_t)s);
+  for (int frag = 0; frag < 2 && !e; ++frag) {
+    if (a->classes & CLS_BIG) e = launch<256, 256, 4, 2, 1, 2, false, BIG_DMA, 64>(a, CLS_BIG, frag, (hipStream_t)s);
+    if (!e && (a->classes & CLS_WIDE))
+      e = launch<256, 320, 4, 2, 1, 1, WIDE_SHARE, WIDE_DMA, WIDE_BKD>(a, CLS_WIDE, frag, (hipStream_t)s);
+    if (!e && (a->classes & CLS_THIN)) e = launch<32, 256, 1, 8, 2, 2>(a, CLS_THIN, frag, (hipStream_t)s);
+  }
   return e;
 }
 
@@ -582,9 +791,11 @@ extern "C" int mli_wgrad_workspace(const mli_wgrad_args* a, int64_t* bytes) {
   if (!a->deterministic) return 0;
   KArgs ka;
   int64_t mx = 0, f;
-  if (a->classes & CLS_BIG) { if ((f = plan<256, 256, 1>(a, CLS_BIG, ka)) < 0) return (int)hipErrorInvalidValue; mx = std::max(mx, f); }
-  if (a->classes & CLS_WIDE) { if ((f = plan<256, 320, 1, WIDE_SHARE>(a, CLS_WIDE, ka)) < 0) return (int)hipErrorInvalidValue; mx = std::max(mx, f); }
-  if (a->classes & CLS_THIN) { if ((f = plan<32, 256, 2>(a, CLS_THIN, ka)) < 0) return (int)hipErrorInvalidValue; mx = std::max(mx, f); }
+  for (int frag = 0; frag < 2; ++frag) {
+    if (a->classes & CLS_BIG) { if ((f = plan<256, 256, 1>(a, CLS_BIG, frag, ka)) < 0) return (int)hipErrorInvalidValue; mx = std::max(mx, f); }
+    if (a->classes & CLS_WIDE) { if ((f = plan<256, 320, 1, WIDE_SHARE>(a, CLS_WIDE, frag, ka)) < 0) return (int)hipErrorInvalidValue; mx = std::max(mx, f); }
+    if (a->classes & CLS_THIN) { if ((f = plan<32, 256, 2>(a, CLS_THIN, frag, ka)) < 0) return (int)hipErrorInvalidValue; mx = std::max(mx, f); }
+  }
   bytes[0] = mx * 4;
   return 0;
 }

@@ -52,6 +52,52 @@ def _grid_levels(cfg):
     return g, total
 
 
+# The scratch buffers a render's geometry writes (rays, the sampling rounds, the FIELD pass):
+# the only ones a training prefetch lane needs of its own (RenderEngine.use_lane(geometry_only)).
+GEOMETRY_BUFS = frozenset(["center", "ray_unit", "ray_norm", "pts_light", "near", "far", "outside",
+                           "d_coarse", "s_coarse", "d_m0", "d_m1", "s_m0", "s_m1", "d_f0", "d_f1", "s_f0",
+                           "s_f1", "dists", "sdf", "grad", "hess", "h0", "enc5"])
+
+
+class _GeometryLane(dict):
+    """A lane's buffer set whose geometry buffers (GEOMETRY_BUFS) are its own and every other
+    buffer (the heads' activations, the backward's dZ images and dW slabs, the loss scratch, the
+    render generation) lives in one set shared by all such lanes.  The training prefetch renders
+    only the geometry of batch k+1 / k+2 into its lane while step k runs, and the steps run one
+    after another on the main stream, so one set of step buffers serves every lane (VERDICT r4
+    item 7: ~7.5 GiB per lane at 4096 x 128 otherwise)."""
+
+    def __init__(self, shared):
+        super().__init__()
+        self.shared = shared
+
+    def _d(self, k):
+        return self if k in GEOMETRY_BUFS else self.shared
+
+    def __getitem__(self, k):
+        d = self._d(k)
+        return dict.__getitem__(d, k) if d is self else d[k]
+
+    def __setitem__(self, k, v):
+        d = self._d(k)
+        if d is self:
+            dict.__setitem__(self, k, v)
+        else:
+            d[k] = v
+
+    def __contains__(self, k):
+        d = self._d(k)
+        return dict.__contains__(d, k) if d is self else k in d
+
+    def get(self, k, default=None):
+        d = self._d(k)
+        return dict.get(d, k, default) if d is self else d.get(k, default)
+
+    def pop(self, k, *default):
+        d = self._d(k)
+        return dict.pop(d, k, *default) if d is self else d.pop(k, *default)
+
+
 def _to_device_structs(structs, device):
     raw = b"".join(bytes(s) for s in structs)
     return torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
@@ -86,6 +132,7 @@ class RenderEngine:
         self.toff = {name: (off, shape) for name, shape, off in self.tlayout}
         self._lanes = {0: {}}
         self._bufs = self._lanes[0]  # the current lane's scratch buffers (see use_lane)
+        self._shared_step = None     # the step buffers shared by the geometry-only lanes
         self.gate_wgrad, self.gate_event = False, None  # event before the dW launches (Trainer.prefetch)
         self.u_fine = (C.c_float * 64)(*(layout.u_fine(cfg.n_fine) + [2.0] * (64 - cfg.n_fine)))
         self._pack_descs = None
@@ -168,11 +215,22 @@ class RenderEngine:
         return flat[off:off + n].reshape(shape)
 
     # ------------------------------------------------------------------ buffers
-    def use_lane(self, lane):
+    def use_lane(self, lane, geometry_only=False):
         """Switch to scratch-buffer set ``lane``: renders in flight on different streams (the
         pipelined inference chunks, Model.inference) each own a buffer set; a lane is reused
-        only on its own stream, so stream order protects it."""
-        self._bufs = self._lanes.setdefault(lane, {})
+        only on its own stream, so stream order protects it.  ``geometry_only`` (the training
+        prefetch lanes, Trainer.prefetch): the lane owns only the geometry buffers and shares the
+        rest with the other such lanes (_GeometryLane)."""
+        if lane not in self._lanes:
+            if geometry_only:
+                if self._shared_step is None:
+                    self._shared_step = {}
+                self._lanes[lane] = _GeometryLane(self._shared_step)
+            else:
+                self._lanes[lane] = {}
+        self._bufs = self._lanes[lane]
+        if geometry_only != isinstance(self._bufs, _GeometryLane):
+            raise RuntimeError("engine lane %r was created with geometry_only=%s" % (lane, not geometry_only))
 
     def _buf(self, name, shape, dtype=torch.float32):
         t = self._bufs.get(name)
@@ -291,8 +349,10 @@ class RenderEngine:
         y = self._buf("y", (N, R, 8))
         if nh == 1:
             y.zero_()  # o_r / o_s slots the single head does not write (composite reads them)
-        feat = self._buf("feat", (S * 256,), torch.float16)
-        x0T = xT = masks = w = q4 = None
+        # the x0 image: SDF feature (k-steps 0..15 of each 32-sample tile) + in training the extras
+        # (16..18); the WIDE dW operand (ABI 15)
+        feat = self._buf("feat", (S * layout.K0,), torch.float16)
+        xT = masks = w = q4 = None
         pq = s_var is not None and self.pq_mode(N, training)
         if training and self.stage == "b" and not self.deterministic:
             # the split-K dW accumulators of this lane's backward, zeroed here at the start of the
@@ -301,8 +361,7 @@ class RenderEngine:
             self._buf("dw", (self._dw_total(),)).zero_()
             self._bufs["dw_clean"] = True
         if training:
-            x0T = self._buf("x0T", (layout.K0, S), torch.float16)
-            xT = self._buf("xT", (nh, 3 if pq else 4, 256, S), torch.float16)
+            xT = self._buf("xT", (nh, 3 if pq else 4, S * 256), torch.float16)  # ACC frag images
             masks = self._buf("masks", (nh, 4, S // 32, 64, 4), torch.int32)
         if pq:
             w = self.weights(rays, dists, fld, s_var, progress)
@@ -310,8 +369,8 @@ class RenderEngine:
         L.call("mli_rgb_fwd", L.RgbFwdArgs(R, N, L.ptr(rays["center"]), L.ptr(rays["ray_unit"]),
                                            L.ptr(rays["pts_light"]), L.ptr(dists), L.ptr(fld["grad"]),
                                            L.ptr(fld["h0"]), L.ptr(self.wfwd), L.ptr(y), L.ptr(feat),
-                                           L.ptr(x0T), L.ptr(xT), L.ptr(masks), nh, L.ptr(w), L.ptr(q4)))
-        return dict(y=y, x0T=x0T, xT=xT, masks=masks, feat=feat, q4=q4)
+                                           L.ptr(xT), L.ptr(masks), nh, L.ptr(w), L.ptr(q4)))
+        return dict(y=y, x0T=feat if training else None, xT=xT, masks=masks, feat=feat, q4=q4)
 
     @torch.no_grad()
     def composite(self, rays, dists, fld, hd, s_var, progress, training):
@@ -468,16 +527,19 @@ class RenderEngine:
                 dw = dwbuf[off:off + m * k]
                 db = dwbuf[off + m * k:off + m * k + m]
                 off += m * k + m
+                # every operand is a fragment image (ABI 15): 16 k-steps per 32-sample tile, the
+                # x0 image 19, dZ4 1
                 if li == 0:
-                    jobs.append(L.WgradJob(L.ptr(dzT[hdx, 0]), L.ptr(hd["x0T"]), m, k, L.ptr(dw), L.ptr(db), k, 1, 1))
+                    jobs.append(L.frag_job(L.ptr(dzT[hdx, 0]), L.ptr(hd["x0T"]), m, k, L.ptr(dw), L.ptr(db), k, 16,
+                                           layout.K0 // 16))
                 elif li < 4:
-                    jobs.append(L.WgradJob(L.ptr(dzT[hdx, li]), L.ptr(hd["xT"][hdx, li - 1]), m, k, L.ptr(dw),
-                                           L.ptr(db), k, 1, 1))
+                    jobs.append(L.frag_job(L.ptr(dzT[hdx, li]), L.ptr(hd["xT"][hdx, li - 1]), m, k, L.ptr(dw),
+                                           L.ptr(db), k, 16, 16))
                 elif pq:
                     dw4[hdx], db4[hdx], k4[hdx] = L.ptr(dw), L.ptr(db), m
                 else:
-                    jobs.append(L.WgradJob(L.ptr(dz4T[hdx]), L.ptr(hd["xT"][hdx, 3]), m, k, L.ptr(dw), L.ptr(db), k,
-                                           0, 1))
+                    jobs.append(L.frag_job(L.ptr(dz4T[hdx]), L.ptr(hd["xT"][hdx, 3]), m, k, L.ptr(dw), L.ptr(db), k,
+                                           1, 16))
                 pre = layout.param_prefix(name, li)
                 v = self.param_view(flat, pre + ".weight_v")
                 g = self.param_view(flat, pre + ".weight_g")
@@ -524,11 +586,11 @@ class RenderEngine:
                                                            L.ptr(c(d_o_r)), L.ptr(c(d_o_s)), L.ptr(c(d_o_re)),
                                                            scale, L.ptr(dz4),
                                                            L.ptr(self._buf("dray", (R, 8)) if pq else None)))
-        dz4T = None if pq else self._buf("dz4T", (3, 4, S), torch.float16)
+        dz4T = None if pq else self._buf("dz4T", (3, S * 16), torch.float16)  # one-k-step frag images
         dwbuf = self._buf("dw", (self._dw_total(),))
         if not self.deterministic and not self._bufs.pop("dw_clean", False):
             dwbuf.zero_()  # split-K partials add into it (fp32 atomics); heads() zeroes it once per render
-        dzT = self._buf("dzT", (3, 4, 256, S), torch.float16)
+        dzT = self._buf("dzT", (3, 4, S * 256), torch.float16)  # ACC frag images
         L.call("mli_rgb_bwd", L.RgbBwdArgs(R, N, L.ptr(dz4), L.ptr(self.wbwd), L.ptr(hd["masks"]), L.ptr(dzT),
                                            L.ptr(dz4T)))
         jobs, ad, (dw4, db4, k4) = self._wgrad_plan(dzT, dz4T, hd, dwbuf, flat, grad_out, S)
@@ -574,8 +636,9 @@ class RenderEngine:
             w, b = take(m, k)
             a_rows = bufs["dzT"][li] if li < 4 else bufs["dz4T"]
             b_rows = bufs["x0T"] if li == 0 else bufs["xT"][0, li - 1]
-            # dZ0..dZ3 and X: tile-blocked images; dZ4 rows are feature-major
-            jobs_s.append(L.WgradJob(L.ptr(a_rows), L.ptr(b_rows), m, k, L.ptr(w), L.ptr(b), k, 1 if li < 4 else 0, 1))
+            # fragment images (ABI 15): dZ0..dZ3 / X 16 k-steps per tile, x0 19, dZ4 1
+            jobs_s.append(L.frag_job(L.ptr(a_rows), L.ptr(b_rows), m, k, L.ptr(w), L.ptr(b), k, 16 if li < 4 else 1,
+                                     layout.K0 // 16 if li == 0 else 16))
             pre = layout.param_prefix(head, li)
             k_ref = pv(pre + ".weight_v").shape[1]
             kinv = layout.head_kinv(head, k_ref) if li == 0 else np.arange(k_ref)
@@ -585,7 +648,8 @@ class RenderEngine:
             keep.append(kt)
         # neural_sdf.mlp.linears.1: dZ1sdf x h0 (S samples)
         w, b = take(256, 256)
-        jobs_s.append(L.WgradJob(L.ptr(bufs["dz1T"]), L.ptr(bufs["h0_rows"]), 256, 256, L.ptr(w), L.ptr(b), 256, 1, 0))
+        # dZ1sdf and the FIELD's h0 image (ACC order, as the heads read it): both fragment images
+        jobs_s.append(L.frag_job(L.ptr(bufs["dz1T"]), L.ptr(bufs["h0"]), 256, 256, L.ptr(w), L.ptr(b), 256, 16, 16))
         pre = "neural_sdf.mlp.linears.1"
         d, kt = self._assemble_desc(w, b, pv(pre + ".weight_v"), pv(pre + ".weight_g"), 256, 256, 256,
                                     np.arange(256), gv(pre + ".weight_v"), gv(pre + ".weight_g"), gv(pre + ".bias"))
@@ -635,9 +699,9 @@ class RenderEngine:
             R, N, L.ptr(dists), L.ptr(rays["far"]), L.ptr(rays["ray_unit"]), L.ptr(fld["sdf"]), L.ptr(fld["grad"]),
             L.ptr(hd["y"]), L.ptr(s_var), float(anneal), 1 if self.cfg.white_bg else 0, L.ptr(d_rgb.contiguous()),
             scale, L.ptr(dz4), L.ptr(d_sdf), L.ptr(d_grad), L.ptr(dinv), L.ptr(self.param_view(grad_flat, "s_var"))))
-        b = dict(dzT=self._buf("dzT", (4, 256, S), f16), dz4T=self._buf("dz4T", (4, S), f16),
-                 x0T=hd["x0T"], xT=hd["xT"], dz1T=self._buf("dz1T", (256, S), f16),
-                 h0_rows=self._buf("h0_rows", (256, S), f16), dz0_rows=self._buf("dz0_rows", (256, 5 * S), f16),
+        b = dict(dzT=self._buf("dzT", (4, 256 * S), f16), dz4T=self._buf("dz4T", (16 * S,), f16),
+                 x0T=hd["x0T"], xT=hd["xT"], dz1T=self._buf("dz1T", (256 * S,), f16),
+                 h0=fld["h0"], dz0_rows=self._buf("dz0_rows", (256, 5 * S), f16),
                  x0_rows=self._buf("x0_rows", (layout.SDF_K0, 5 * S), f16), dws=self._buf("dws", (257,)))
         d_nrm = self._buf("d_nrm", (N, R, 4))
         dh0 = self._buf("dh0", (S * 256,), f16)
@@ -663,8 +727,7 @@ class RenderEngine:
         L.call("mli_hash_bwd", L.HashBwdArgs(R, N, L.ptr(rays["center"]), L.ptr(rays["ray_unit"]), L.ptr(dists),
                                              L.ptr(d_enc), self.levels, self.eps, int(self.active_levels),
                                              L.ptr(grad_table), det, L.ptr(hws), grad_table.numel()))
-        # feature-major operand rows of the SDF weight gradients
-        L.call("mli_frag_rows", L.FragRowsArgs(L.ptr(fld["h0"]), 16 * 512, T, 16, 1, L.ptr(b["h0_rows"]), S, 0, 0))
+        # feature-major operand rows of the SDF layer-0 weight gradient (5S samples)
         for pi in range(5):
             L.call("mli_frag_rows", L.FragRowsArgs(L.ptr(fld["enc"]) + pi * 8 * 512 * 2, 5 * 8 * 512, T, 8, 0,
                                                    L.ptr(b["x0_rows"]), 5 * S, pi * S, 3))

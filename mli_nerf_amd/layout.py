@@ -173,3 +173,52 @@ def untile(img, rows):
     flat = img.reshape(-1)
     S = flat.numel() // rows
     return flat.view(S // 256, rows, 256).permute(1, 0, 2).reshape(rows, S)
+
+
+def unfrag(img, rows, kst=None, order="acc"):
+    """A fragment image ([S/32][kst][64 lanes][8 halves], include/mli_hip.h ABI 15; ``kst`` k-steps
+    per 32-sample tile, default rows / 16) as feature-major rows [rows][S] (a copy, for
+    inspection and tests).  Element j of lane c + 32 h of k-step q is sample c of the tile and
+    feature 16 q + 8 (j >> 2) + 4 h + (j & 3) (ACC order) or 16 q + 8 h + j (NAT order)."""
+    kst = kst or (rows + 15) // 16
+    flat = img.reshape(-1)
+    S = flat.numel() // (kst * 16)
+    x = flat.view(S // 32, kst, 2, 32, 2, 4) if order == "acc" else flat.view(S // 32, kst, 2, 32, 8)
+    if order == "acc":
+        # dims (tile, q, h, c, j>>2, j&3) -> feature 16 q + 8 (j>>2) + 4 h + (j&3)
+        x = x.permute(1, 4, 2, 5, 0, 3)       # (q, j>>2, h, j&3, tile, c)
+    else:
+        x = x.permute(1, 2, 4, 0, 3)          # (q, h, j, tile, c)
+    return x.reshape(kst * 16, S)[:rows]
+
+
+def frag_index(m, f, kst, order="acc"):
+    """Element offset of (sample m, feature f) in a fragment image with kst k-steps per tile
+    (the index rule of include/mli_hip.h, for tests)."""
+    q, r = divmod(f, 16)
+    if order == "acc":
+        h, j = (r >> 2) & 1, ((r >> 3) << 2) | (r & 3)
+    else:
+        h, j = r >> 3, r & 7
+    return ((m // 32) * kst + q) * 512 + ((m % 32) + 32 * h) * 8 + j
+
+
+def to_frag(rows, kst=None, order="acc"):
+    """Feature-major rows [rows][S] (S % 32 == 0) as a fragment image with ``kst`` k-steps per
+    tile (rows past the matrix zero): the inverse of unfrag (tests)."""
+    import torch
+    n, S = rows.shape
+    kst = kst or (n + 15) // 16
+    full = torch.zeros(kst * 16, S, dtype=rows.dtype, device=rows.device)
+    full[:n] = rows
+    if order == "acc":
+        x = full.view(kst, 2, 2, 4, S // 32, 32).permute(4, 0, 2, 5, 1, 3)   # (tile, q, h, c, j>>2, j&3)
+    else:
+        x = full.view(kst, 2, 8, S // 32, 32).permute(3, 0, 1, 4, 2)         # (tile, q, h, c, j)
+    return x.contiguous().reshape(-1)
+
+
+def to_tiled(rows):
+    """Feature-major rows [rows][S] (S % 256 == 0) as a tile-blocked image: inverse of untile."""
+    n, S = rows.shape
+    return rows.view(n, S // 256, 256).permute(1, 0, 2).contiguous().reshape(-1)

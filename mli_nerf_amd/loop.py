@@ -26,29 +26,38 @@ def _get(cfg, path, default=None):
     return default if node is None else node
 
 
-def make_data_loader(cfg, split, shuffle=True, seed=0):
-    """imaginaire/utils/dataset.py get_train/val_dataloader, one process: the project's Dataset
-    (this build's ``mli_nerf_amd.data.Dataset``, both NeuralLumen layouts) in a torch DataLoader
-    with the config's batch size; under a process group a DistributedSampler shards it."""
+def make_data_loader(cfg, split, shuffle=True, seed=0, drop_last=None, subset_indices=None):
+    """imaginaire/datasets/utils/get_dataloader.py get_train/val/test_dataloader, one process: the
+    project's Dataset (this build's ``mli_nerf_amd.data.Dataset``, both NeuralLumen layouts),
+    restricted to ``subset_indices`` by a torch Subset (get_dataloader.py:35-36,56-57), in a torch
+    DataLoader with the config's batch size; under a process group a DistributedSampler shards it.
+    ``drop_last`` defaults to the split's (train: True)."""
     from .data import Dataset
     ds = Dataset(cfg, is_inference=split != "train", is_test=split == "test")
+    if subset_indices is not None:
+        ds = torch.utils.data.Subset(ds, subset_indices)
     bs = int(_get(cfg, "data.%s.batch_size" % ("train" if split == "train" else "val"), 1) or 1)
     sampler = None
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():
         sampler = torch.utils.data.distributed.DistributedSampler(ds, shuffle=shuffle and split == "train", seed=seed)
     g = torch.Generator().manual_seed(seed)
+    if drop_last is None:
+        drop_last = split == "train"
     return torch.utils.data.DataLoader(ds, batch_size=bs, shuffle=(shuffle and split == "train" and sampler is None),
-                                       sampler=sampler, drop_last=split == "train", generator=g, num_workers=0)
+                                       sampler=sampler, drop_last=drop_last, generator=g, num_workers=0)
 
 
 def set_data_loader(trainer, cfg, split, shuffle=True, drop_last=True, seed=0, subset_indices=None):
-    """imaginaire/trainers/base.py:87-101."""
+    """imaginaire/trainers/base.py:87-101: ``drop_last`` applies to the training split,
+    ``subset_indices`` to the validation split, as there."""
     assert split in ("train", "val", "test")
     if split == "train":
-        trainer.train_data_loader = make_data_loader(cfg, "train", shuffle, seed)
+        trainer.train_data_loader = make_data_loader(cfg, "train", shuffle, seed, drop_last=drop_last)
+    elif split == "val":
+        trainer.eval_data_loader = make_data_loader(cfg, "val", False, seed, subset_indices=subset_indices)
     else:
-        trainer.eval_data_loader = make_data_loader(cfg, split, False, seed)
+        trainer.eval_data_loader = make_data_loader(cfg, "test", False, seed)
 
 
 def end_of_iteration(trainer, current_epoch, current_iteration):
@@ -64,8 +73,22 @@ def end_of_iteration(trainer, current_epoch, current_iteration):
         trainer.checkpointer.save(current_epoch, current_iteration, True)
 
 
+def _profiler(enabled):
+    """base.py:501-504: torch.autograd.profiler.profile(use_cuda, profile_memory, record_shapes)
+    around an iteration when ``--profile``; here torch.profiler with the CPU + GPU (HIP) activities,
+    whose trace also carries the libmli_hip.so kernels."""
+    import contextlib
+    if not enabled:
+        return contextlib.nullcontext()
+    from torch.profiler import ProfilerActivity, profile
+    acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if torch.cuda.is_available() else [])
+    return profile(activities=acts, profile_memory=True, record_shapes=True)
+
+
 def train(trainer, cfg, data_loader, single_gpu=False, profile=False, show_pbar=False):
-    """base.py:474-527 (+ neuralangelo/trainer.py:110-112: the progress at the start)."""
+    """base.py:474-527 (+ neuralangelo/trainer.py:110-112: the progress at the start).  With
+    ``profile`` each iteration runs under the profiler, whose table is printed and whose chrome
+    trace goes to <logdir>/trace.json (base.py:501-521)."""
     start_epoch = trainer.checkpointer.resume_epoch or trainer.current_epoch
     it = trainer.checkpointer.resume_iteration or trainer.current_iteration
     trainer.model.progress = it / cfg.max_iter
@@ -77,11 +100,19 @@ def train(trainer, cfg, data_loader, single_gpu=False, profile=False, show_pbar=
         trainer.current_epoch = epoch
         n = len(data_loader)
         for i, data in enumerate(data_loader):
-            data = trainer.start_of_iteration(data, it)
-            trainer.train_step(data, last_iter_in_epoch=(i == n - 1))
-            it += 1
-            end_of_iteration(trainer, epoch + 1 if i == n - 1 else epoch, it)
-            if it >= cfg.max_iter:
+            with _profiler(profile) as prof:
+                data = trainer.start_of_iteration(data, it)
+                trainer.train_step(data, last_iter_in_epoch=(i == n - 1))
+                it += 1
+                end_of_iteration(trainer, epoch + 1 if i == n - 1 else epoch, it)
+                done = it >= cfg.max_iter
+            if profile:
+                sort = "cuda_time_total" if torch.cuda.is_available() else "cpu_time_total"
+                print(prof.key_averages().table(sort_by=sort, row_limit=20))
+                logdir = _get(cfg, "logdir", ".") or "."
+                os.makedirs(logdir, exist_ok=True)
+                prof.export_chrome_trace(os.path.join(logdir, "trace.json"))
+            if done:
                 print("Done with training!!!")
                 return
         save_epoch = int(_get(cfg, "checkpoint.save_epoch", 0) or 0)

@@ -193,6 +193,109 @@ def reduce_and_step_table(optim, grad, lr, p16, world_size, chunk, overlap=True,
     optim.step(grad, lr, p16=p16, ranges=chunks, before=ready)
 
 
+class ZeroTableAdamW:
+    """Stage a over several ranks, ZeRO-style: the hash table's AdamW state is
+    sharded.  Rank r owns table elements [lo, hi) = [r * per, (r + 1) * per) (per = ceil(n / world);
+    the gradient and fp16-shadow buffers are padded to world * per):
+
+      reduce-scatter of the table gradient -> this rank's shard of the sum, / world
+      -> AdamW on the shard (fp32 master slice, shard-sized moments, the fp16 shadow slice)
+      -> all-gather of the fp16 gather shadow only (what every rank's kernels read).
+
+    Per rank that moves (w-1)/w x (4 B + 2 B) per element instead of the all-reduce's
+    2 (w-1)/w x 4 B, and runs 1/w of the 11 GB AdamW pass.  The fp32 master outside [lo, hi) and
+    the moments are only gathered for a checkpoint (sync(), a collective every rank calls: the
+    file layout is that of the unsharded run).  Every element sees the serial path's operations
+    (its rank sum, / world, the element-wise update); at world size 2 the sums are exact in any
+    order, so the sharded and serial steps are bit-identical (tests/test_distributed.py)."""
+
+    def __init__(self, table, world_size, rank, lr=1e-3, weight_decay=1e-2, group=None):
+        self.table, self.world, self.rank, self.group = table, world_size, rank, group
+        self.lr, self.wd = lr, weight_decay
+        self._shard(table.numel())
+        self.p16_pad = None     # [world * per] fp16; the engine's table16 is its [:n] view
+
+    def _shard(self, n):
+        self.n = n
+        self.per = -(-n // self.world)
+        self.lo = min(n, self.rank * self.per)
+        self.hi = min(n, self.lo + self.per)
+        self.optim = FusedAdamW(self.table.detach()[self.lo:self.hi], lr=self.lr, weight_decay=self.wd)
+        self.gshard = torch.zeros(self.per, device=self.table.device)
+
+    @property
+    def step_count(self):
+        return self.optim.step_count
+
+    @step_count.setter
+    def step_count(self, k):
+        self.optim.step_count = k
+
+    @property
+    def m(self):
+        return self.optim.m
+
+    @property
+    def v(self):
+        return self.optim.v
+
+    def resize(self, numel):
+        """A table of another size rule (Model.load_state_dict): new shards, zero moments."""
+        if numel != self.n:
+            k = self.optim.step_count
+            self._shard(numel)
+            self.optim.step_count = k
+            self.p16_pad = None
+
+    def padded_grad(self, cur=None):
+        """A [world * per] gradient buffer; the engine writes its [:n] view."""
+        if cur is None or cur.numel() != self.world * self.per or cur.device != self.table.device:
+            cur = torch.zeros(self.world * self.per, device=self.table.device)
+        return cur
+
+    def bind_shadow(self, engine):
+        """Make the engine's fp16 gather shadow a view of the padded all-gather target."""
+        t16 = engine.table16
+        if self.p16_pad is not None and t16 is not None and t16.data_ptr() == self.p16_pad.data_ptr() \
+                and t16.numel() == self.n:
+            return
+        pad = torch.zeros(self.world * self.per, dtype=torch.float16, device=self.table.device)
+        if t16 is not None and t16.numel() == self.n:
+            pad[:self.n].copy_(t16)
+        self.p16_pad = pad
+        engine.table16 = pad[:self.n]
+
+    def step(self, grad_pad, lr):
+        import torch.distributed as dist
+        dist.reduce_scatter_tensor(self.gshard, grad_pad, op=dist.ReduceOp.SUM, group=self.group)
+        k = self.hi - self.lo
+        g = self.gshard[:k]
+        g.div_(self.world)
+        self.optim.step(g, lr, p16=self.p16_pad[self.lo:self.hi])
+        mine = self.p16_pad[self.rank * self.per:(self.rank + 1) * self.per]
+        dist.all_gather_into_tensor(self.p16_pad, mine, group=self.group)
+
+    def _gather(self, shard):
+        import torch.distributed as dist
+        buf = torch.zeros(self.per, dtype=shard.dtype, device=shard.device)
+        buf[:shard.numel()] = shard
+        full = torch.empty(self.world * self.per, dtype=shard.dtype, device=shard.device)
+        dist.all_gather_into_tensor(full, buf, group=self.group)
+        return full[:self.n]
+
+    def sync(self):
+        """Collective (every rank): the fp32 master gathered into the table parameter; returns the
+        full moments (exp_avg, exp_avg_sq) for the optimizer state dict."""
+        t = self.table.detach()
+        t.copy_(self._gather(t[self.lo:self.hi].clone()))
+        return self._gather(self.optim.m), self._gather(self.optim.v)
+
+    def load_full(self, m_full, v_full):
+        """Moments of the unsharded layout (a checkpoint): this rank's slice."""
+        self.optim.m.copy_(m_full.reshape(-1)[self.lo:self.hi])
+        self.optim.v.copy_(v_full.reshape(-1)[self.lo:self.hi])
+
+
 class Checkpointer:
     """imaginaire/trainers/base.py:557-687 surface over the Trainer's checkpoint layout:
     ``trainer.checkpointer.load(path, resume, load_opt=..., load_sch=...)`` as test.py:93 calls
@@ -247,6 +350,7 @@ class Checkpointer:
         import torch.distributed as dist
         tr = self.trainer
         tr.current_epoch, tr.current_iteration = current_epoch, current_iteration
+        tr.sync_table()   # ZeRO table (stage a, several ranks): a collective every rank takes part in
         if dist.is_available() and dist.is_initialized() and dist.get_rank() != 0:
             name = "latest_checkpoint.pt" if latest else \
                 "epoch_{:05}_iteration_{:09}_checkpoint.pt".format(current_epoch, current_iteration)
@@ -295,9 +399,22 @@ class Trainer:
         if not is_inference:
             self.optim = FusedAdamW(model.flat, lr=o.params.lr, weight_decay=o.params.weight_decay)
             if self.stage == "a":
-                # stage a trains the hash table too (one AdamW group, NeuralLumen/model.py:422-438)
-                self.optim_table = FusedAdamW(model.neural_sdf.tcnn_encoding.params, lr=o.params.lr,
-                                              weight_decay=o.params.weight_decay)
+                # stage a trains the hash table too (one AdamW group, NeuralLumen/model.py:422-438);
+                # over several ranks its optimizer state is sharded (ZeroTableAdamW) unless the
+                # deterministic mode keeps the single all-reduce (cfg.trainer.zero_table: False
+                # forces the replicated form)
+                zero = cfg.trainer.get("zero_table", None)
+                if zero is None:
+                    zero = world_size > 1 and not model.deterministic
+                if zero and world_size > 1:
+                    import torch.distributed as dist
+                    self.optim_table = ZeroTableAdamW(model.neural_sdf.tcnn_encoding.params, world_size,
+                                                      dist.get_rank(), lr=o.params.lr,
+                                                      weight_decay=o.params.weight_decay)
+                else:
+                    self.optim_table = FusedAdamW(model.neural_sdf.tcnn_encoding.params, lr=o.params.lr,
+                                                  weight_decay=o.params.weight_decay)
+        self._table_full_moments = None   # ZeRO: the gathered moments of the last sync_table()
         if self.stage == "a":
             self.init_curvature = float(cfg.trainer.loss_weight.get("curvature", 0.0))
             if model.neural_sdf.c2f is not None:   # neuralangelo/trainer.py:30-32
@@ -337,11 +454,11 @@ class Trainer:
         """The lanes rotate modulo depth + 1: a change while prefetched batches are pending could
         point the next prefetch at a lane still in use, so it is refused then.
 
-        Memory: the prefetch runs the whole step inside its lane's buffer set, so each lane holds a
-        full set of per-step buffers (activations xT / x0T / feat, dZ, masks, the encoding image,
-        the dW slabs): about 7.5 GiB per lane at 4096 x 128 samples and about 22 GiB at the
-        reference's 8192 x 192 -- depth 2 (three lanes) is affordable on the 288 GB of an MI355X,
-        and bench.py reports the allocator's peak as ``hbm_peak_gib``."""
+        Memory: a prefetch lane holds only the geometry of its batch (rays, the sampling rounds,
+        the FIELD pass: sdf / grad / hess, the h0 and encoding images); the step's buffers
+        (activations, dZ images, masks, dW slabs) are one set shared by the lanes
+        (engine._GeometryLane), since the steps themselves run one after another on the main
+        stream.  bench.py reports the allocator's peak as ``hbm_peak_gib``."""
         d = int(d)
         if d < 1:
             raise ValueError("prefetch_depth must be >= 1")
@@ -412,6 +529,49 @@ class Trainer:
         full = ranges == [(0, self.model.flat.numel())]
         self._ranges_key, self._ranges = key, None if full else ranges
         return self._ranges
+
+    def _step_flat(self, grad, lr):
+        """The fused AdamW over adam_ranges(); the optimized Parameters it stepped are recorded
+        (``stepped``), so a parameter stepped earlier and frozen later keeps its moments in the
+        optimizer state dict, as torch AdamW keeps them."""
+        self.optim.step(grad, lr, ranges=self.adam_ranges())
+        key = getattr(self, "_ranges_key", None)
+        if getattr(self, "_stepped_key", None) != key:
+            self._stepped_key = key
+            self.stepped.update(n for n, p in self._optimized_cached() if p.requires_grad)
+
+    @property
+    def stepped(self):
+        """Names of the optimized Parameters an optimizer step has updated (or whose moments a
+        loaded optimizer state holds)."""
+        if getattr(self, "_stepped", None) is None:
+            self._stepped = set()
+        return self._stepped
+
+    def _step_table(self, grad, lr):
+        """The table's averaged-gradient AdamW step: sharded (ZeroTableAdamW) or replicated
+        (reduce_and_step_table: one all-reduce, or chunks overlapped with their AdamW)."""
+        eng = self.model.engine
+        if isinstance(self.optim_table, ZeroTableAdamW):
+            z = self.optim_table
+            z.bind_shadow(eng)
+            pad = getattr(self, "_grad_table_pad", None)
+            if pad is None or grad.data_ptr() != pad.data_ptr():   # (the autograd path's table.grad)
+                pad = self._grad_table_pad = z.padded_grad(pad)
+                pad[:grad.numel()].copy_(grad.reshape(-1))
+            z.step(pad, lr)
+            self._table_synced = False
+            return
+        reduce_and_step_table(self.optim_table, grad, lr, eng.table16, self.world_size, self.table_chunk,
+                              overlap=self._table_overlap())
+
+    def sync_table(self):
+        """ZeRO table: gather the fp32 master and the moments (a collective: every rank calls it,
+        Checkpointer.save does) so that state_dict / the optimizer state are the unsharded ones.
+        A no-op otherwise."""
+        if isinstance(self.optim_table, ZeroTableAdamW) and not getattr(self, "_table_synced", True):
+            self._table_full_moments = self.optim_table.sync()
+            self._table_synced = True
 
     def _table_overlap(self):
         return (not self.model.deterministic) if self.table_overlap is None else bool(self.table_overlap)
@@ -505,7 +665,7 @@ class Trainer:
             with torch.cuda.stream(side):
                 for k in ("ray_idx", "pose", "intr", "pose_light"):
                     data[k].record_stream(side)
-                eng.use_lane(lane)
+                eng.use_lane(lane, geometry_only=True)
                 rays = eng.rays(data["pose"], data["intr"], data["pose_light"], data["ray_idx"],
                                 m.image_size_train[1])
                 dists = eng.sample(rays, m.stratified_uniforms(data, u))
@@ -585,7 +745,7 @@ class Trainer:
         else:
             lane, rays, dists, fld, done = pf
             torch.cuda.current_stream(m.flat.device).wait_event(done)
-            eng.use_lane(lane)
+            eng.use_lane(lane, geometry_only=True)
             hd = eng.heads(rays, dists, fld, True, m.s_var.detach(), m.progress)
             comp = None if fused else eng.composite(rays, dists, fld, hd, m.s_var.detach(), m.progress, True)
             st = (rays, dists, fld, hd, comp)
@@ -616,7 +776,7 @@ class Trainer:
             self._gate_ev, eng.gate_event = eng.gate_event, None
         reduce_gradients(self._grad, self.world_size)   # gradients + metrics, one collective
         m.set_flat_grad(grad)
-        self.optim.step(grad, self.lr(), ranges=self.adam_ranges())
+        self._step_flat(grad, self.lr())
         self.current_iteration += 1
         self._publish(lv)
         return m.outputs(st) if return_outputs else None
@@ -669,7 +829,10 @@ class Trainer:
         grad, lv = self._grad_buffer()
         d_rgb = self._fused_losses(st, data, lv)[0]
         table = m.neural_sdf.tcnn_encoding.params
-        if self._grad_table is None or self._grad_table.device != table.device or \
+        if isinstance(self.optim_table, ZeroTableAdamW):
+            self._grad_table_pad = self.optim_table.padded_grad(getattr(self, "_grad_table_pad", None))
+            self._grad_table = self._grad_table_pad[:table.numel()]
+        elif self._grad_table is None or self._grad_table.device != table.device or \
                 self._grad_table.numel() != table.numel():
             self._grad_table = torch.empty_like(table.detach())
         m.engine.backward_a(st, d_rgb, m.flat.detach(), grad, self._grad_table,
@@ -688,11 +851,10 @@ class Trainer:
         reduce_gradients(self._grad, self.world_size)
         m.set_flat_grad(grad)
         lr = self.lr()
-        self.optim.step(grad, lr, ranges=self.adam_ranges())
+        self._step_flat(grad, lr)
         if self.table_trains():
             # (a frozen table needs no averaged gradient: no collective for it)
-            reduce_and_step_table(self.optim_table, self._grad_table, lr, eng.table16, self.world_size,
-                                  self.table_chunk, overlap=self._table_overlap())
+            self._step_table(self._grad_table, lr)
         self.current_iteration += 1
         self._publish(lv)
         return m.outputs(st) if return_outputs else None
@@ -722,11 +884,9 @@ class Trainer:
         lv[5], lv[6] = total.detach(), psnr.detach()
         reduce_gradients(self._grad, self.world_size)
         m.set_flat_grad(grad)
-        self.optim.step(grad, self.lr(), ranges=self.adam_ranges())
+        self._step_flat(grad, self.lr())
         if self.stage == "a" and self.table_trains():
-            table = m.neural_sdf.tcnn_encoding.params
-            reduce_and_step_table(self.optim_table, table.grad, self.lr(), m.engine.table16, self.world_size,
-                                  self.table_chunk, overlap=self._table_overlap())
+            self._step_table(m.neural_sdf.tcnn_encoding.params.grad, self.lr())
         self.current_iteration += 1
         self._publish(lv)
         return out
@@ -747,7 +907,12 @@ class Trainer:
                 off, shape, k = offs[name]
                 out.append((name, p, self.optim.m[off:off + k].view(shape), self.optim.v[off:off + k].view(shape)))
             elif self.optim_table is not None and p is self.model.neural_sdf.tcnn_encoding.params:
-                out.append((name, p, self.optim_table.m, self.optim_table.v))
+                if isinstance(self.optim_table, ZeroTableAdamW):
+                    # the full moments exist only as sync_table() gathered them (None: never stepped)
+                    mv = self._table_full_moments
+                    out.append((name, p, None if mv is None else mv[0], None if mv is None else mv[1]))
+                else:
+                    out.append((name, p, self.optim_table.m, self.optim_table.v))
             else:
                 raise RuntimeError("optimized parameter %s is not trained by this build's optimizer" % name)
         return out
@@ -766,11 +931,19 @@ class Trainer:
                      params=list(range(len(views))))
         state = {}
         if self.optim.step_count > 0:
-            for i, (_, p, m, v) in enumerate(views):
+            stepped = self.stepped | ({"neural_sdf.tcnn_encoding.params"} if self.optim_table is not None and
+                                      self.optim_table.step_count > 0 else set())
+            for i, (name, p, m, v) in enumerate(views):
                 # torch AdamW keeps no state for a parameter it never stepped (grad None: frozen by
                 # partial_grad / partial_training): no entry, so no resume applies a bias
-                # correction to moments that were never accumulated
-                if not p.requires_grad:
+                # correction to moments that were never accumulated.  A parameter stepped earlier
+                # and frozen since keeps its entry (torch keeps its state).
+                if name not in stepped and not p.requires_grad:
+                    continue
+                if m is None:   # ZeRO table never stepped or not gathered (sync_table)
+                    if self.optim_table.step_count > 0:
+                        raise RuntimeError("the sharded table's moments were not gathered: save through "
+                                           "trainer.checkpointer.save (or call sync_table on every rank)")
                     continue
                 state[i] = {"step": torch.tensor(float(self.optim.step_count)),
                             "exp_avg": m.detach().cpu().clone(), "exp_avg_sq": v.detach().cpu().clone()}
@@ -800,6 +973,18 @@ class Trainer:
             step = 0
             for i, (name, p, m, v) in zip(idx, views):
                 st = osd["state"].get(i)
+                zt = isinstance(self.optim_table, ZeroTableAdamW) and p is self.model.neural_sdf.tcnn_encoding.params
+                if zt:   # this rank's slice of the unsharded moments
+                    z = self.optim_table
+                    if st:
+                        z.load_full(st["exp_avg"], st["exp_avg_sq"])
+                        step = int(float(st["step"]))
+                        self.stepped.add(name)
+                    else:
+                        z.m.zero_()
+                        z.v.zero_()
+                    self._table_full_moments, self._table_synced = None, True
+                    continue
                 if not st:
                     m.zero_()
                     v.zero_()
@@ -810,6 +995,7 @@ class Trainer:
                 m.copy_(st["exp_avg"])
                 v.copy_(st["exp_avg_sq"])
                 step = int(float(st["step"]))
+                self.stepped.add(name)
             self.optim.step_count = step
             if self.optim_table is not None:
                 self.optim_table.step_count = step
@@ -826,6 +1012,9 @@ class Trainer:
         os.makedirs(logdir, exist_ok=True)
         name = "latest_checkpoint.pt" if latest else \
             "epoch_{:05}_iteration_{:09}_checkpoint.pt".format(self.current_epoch, self.current_iteration)
+        if not getattr(self, "_table_synced", True):
+            raise RuntimeError("save_checkpoint: the ZeRO-sharded table is not gathered; save through "
+                               "trainer.checkpointer.save (every rank) or call sync_table() on every rank")
         sd = {"module." + k: v.detach().cpu() for k, v in self.model.state_dict().items()}
         ck = dict(model=sd, epoch=self.current_epoch, iteration=self.current_iteration)
         if self.optim is not None:

@@ -97,7 +97,7 @@ def test_workspace_queries_match_engine_buffers():
     assert L.workspace("mli_sdf", L.SdfArgs(1, R, N)) == [(S // 32) * 32 * 640 * f16]
     assert L.workspace("mli_sdf", L.SdfArgs(0, R, 64)) == [0]
     assert L.workspace("mli_rgb_fwd", L.RgbFwdArgs(R, N, n_heads=3)) == [
-        N * R * 8 * f32, S * 256 * f16, layout.K0 * S * f16, 3 * 4 * 256 * S * f16, 3 * 4 * (S // 32) * 64 * 4 * 4, 0]
+        N * R * 8 * f32, layout.K0 * S * f16, 0, 3 * 4 * 256 * S * f16, 3 * 4 * (S // 32) * 64 * 4 * 4, 0]
     # PQ mode (weights set): X3 not stored, the output-layer partials q4 instead
     pq = L.RgbFwdArgs(R, N, n_heads=3)
     pq.weights = 1
@@ -114,9 +114,9 @@ def test_workspace_queries_match_engine_buffers():
     d4.k_out = (C.c_int * 3)(3, 3, 4)   # head 2 has one output slot left in dray
     with pytest.raises(RuntimeError):
         L.workspace("mli_dw4", d4)
-    assert L.workspace("mli_rgb_bwd", L.RgbBwdArgs(R, N)) == [3 * 4 * 256 * S * f16, 3 * 4 * S * f16]
+    assert L.workspace("mli_rgb_bwd", L.RgbBwdArgs(R, N)) == [3 * 4 * 256 * S * f16, 3 * 16 * S * f16]
     assert L.workspace("mli_geo_bwd", L.GeoBwdArgs(R, N)) == [
-        4 * 256 * S * f16, 4 * S * f16, N * R * 4 * f32, 256 * S * f16, S * 256 * f16, 0]
+        4 * 256 * S * f16, 16 * S * f16, N * R * 4 * f32, 256 * S * f16, S * 256 * f16, 0]
     assert L.workspace("mli_composite_bwd_geo", L.CompositeBwdGeoArgs(R, N)) == [
         N * R * 8 * f32, N * R * f32, N * R * 3 * f32, R * f32]
     assert L.workspace("mli_sdf_bwd", L.SdfBwdArgs(R, N)) == [
@@ -129,19 +129,29 @@ def test_workspace_queries_match_engine_buffers():
     assert L.workspace("mli_hash_bwd", L.HashBwdArgs(R, N, deterministic=1, n_params=n_params)) == [n_params * 8]
     assert L.workspace("mli_hash_bwd", L.HashBwdArgs(R, N, n_params=n_params)) == [0]
     # wgrad: the stage-b jobs (engine._wgrad_plan shapes): partial slabs only in deterministic mode
-    jobs = []
-    for name, k_in, k_out in layout.HEADS:
-        for m, k in [(256, layout.K0), (256, 256), (256, 256), (256, 256), (k_out, 256)]:
-            jobs.append(L.WgradJob(None, None, m, k, None, None, k))
-    arr = (L.WgradJob * len(jobs))(*jobs)
-    q = L.WgradArgs(S, len(jobs), C.cast(arr, C.c_void_p), 7, 0, None)
-    assert L.workspace("mli_wgrad", q) == [0]
-    q.deterministic = 1
-    ws = L.workspace("mli_wgrad", q)[0]
-    assert 16 * 2 ** 20 < ws < 512 * 2 ** 20, ws   # tens of MiB of fp32 partial slabs
-    q.S = 100   # not a multiple of the 64-sample k-step
-    with pytest.raises(RuntimeError):
-        L.workspace("mli_wgrad", q)
+    for frag in (False, True):   # rows and (ABI 15) fragment-image operands
+        jobs = []
+        for name, k_in, k_out in layout.HEADS:
+            for m, k in [(256, layout.K0), (256, 256), (256, 256), (256, 256), (k_out, 256)]:
+                if frag:
+                    jobs.append(L.frag_job(None, None, m, k, None, None, k, (m + 15) // 16, (k + 15) // 16))
+                else:
+                    jobs.append(L.WgradJob(None, None, m, k, None, None, k))
+        arr = (L.WgradJob * len(jobs))(*jobs)
+        q = L.WgradArgs(S, len(jobs), C.cast(arr, C.c_void_p), 7, 0, None)
+        assert L.workspace("mli_wgrad", q) == [0]
+        q.deterministic = 1
+        ws = L.workspace("mli_wgrad", q)[0]
+        assert 16 * 2 ** 20 < ws < 512 * 2 ** 20, ws   # tens of MiB of fp32 partial slabs
+        q.S = 100   # not a multiple of the 64-sample k-step
+        with pytest.raises(RuntimeError):
+            L.workspace("mli_wgrad", q)
+    # invalid fragment jobs: one operand a fragment image and the other not; too few k-steps per tile
+    for bad in (L.WgradJob(None, None, 256, 256, None, None, 256, L.FRAG_ACC, L.ROWS, 16, 0),
+                L.frag_job(None, None, 256, 304, None, None, 304, 16, 16)):
+        arr = (L.WgradJob * 1)(bad)
+        with pytest.raises(RuntimeError):
+            L.workspace("mli_wgrad", L.WgradArgs(S, 1, C.cast(arr, C.c_void_p), 7, 1, None))
 
 
 def test_source_hash_detects_stale_library(tmp_path, monkeypatch):
@@ -175,3 +185,29 @@ def test_untile_inverts_the_tile_blocked_layout():
     assert out.shape == (rows, S)
     for r, m in ((0, 0), (3, 517), (4, 767), (1, 255), (2, 256)):
         assert out[r, m].item() == (m // 256) * rows * 256 + r * 256 + m % 256
+
+
+def test_unfrag_inverts_the_fragment_layout():
+    """layout.unfrag (the host's view of the ABI 15 fragment images) against the index rule
+    include/mli_hip.h states, ACC and NAT order, with a tile stride above rows / 16."""
+    import torch
+    from mli_nerf_amd import layout
+    for order in ("acc", "nat"):
+        rows, kst, S = 40, 4, 96
+        img = torch.arange(S * kst * 16, dtype=torch.int64)
+        out = layout.unfrag(img, rows, kst, order)
+        assert out.shape == (rows, S)
+        for f in range(rows):
+            for m in (0, 5, 31, 32, 63, 95):
+                assert out[f, m].item() == layout.frag_index(m, f, kst, order), (order, f, m)
+        assert torch.equal(layout.unfrag(layout.to_frag(out, kst, order), rows, kst, order), out)
+    t = torch.arange(3 * 512).view(3, 512)
+    assert torch.equal(layout.untile(layout.to_tiled(t), 3), t)
+    # ACC order is what acc_to_frag() stores: element j of lane half h is accumulator row
+    # acc_row(8 s + j, h) of k-step 2t + s (mlp_core.h / common.h)
+    acc_row = lambda i, h: (i & 3) + 8 * (i >> 2) + 4 * h  # noqa: E731
+    for s in (0, 1):
+        for h in (0, 1):
+            for j in range(8):
+                f = acc_row(8 * s + j, h)
+                assert layout.frag_index(0, f, 2) == (s * 512 + 32 * h * 8 + j), (s, h, j)

@@ -1,6 +1,6 @@
-"""The training images the heads forward stores for the weight gradients (ABI 14 tile-blocked
-``[S/256][rows][256]`` x0T and X1..X3, read back through ``layout.untile``) against the oracle's
-activations at the same samples.
+"""The training images the heads forward stores for the weight gradients (ABI 15 fragment images
+``[S/32][k-steps][64][8]`` in ACC order: the x0 image -- 19 k-steps per tile -- and X1..X3, read
+back through ``layout.unfrag``) against the oracle's activations at the same samples.
 
 x0T rows: 0..255 the SDF feature (layer 1 of the SDF MLP, fp16 MFMA against the fp32 oracle:
 4e-3 of its range), 256..258 the point, 259..261 the normal, 262..271 zero padding, 272..287 SH16
@@ -34,7 +34,7 @@ def test_stored_activations_match_oracle():
     c_g, v_g = rays["center"].cpu()[None], rays["ray_unit"].cpu()[None]
     pts = c_g[..., None, :] + v_g[..., None, :] * d_g
     _, feat = o_render.sdf_net(fp16_table_sd(sd), pcfg, pts, with_feat=True)   # [1, R, N, 256]
-    x0T = layout.untile(hd["x0T"], layout.K0).float().cpu()                    # [304][S], tile order
+    x0T = layout.unfrag(hd["x0T"], layout.K0).float().cpu()                    # [304][S], tile order
     feat_t = feat[0].reshape(S, 256).t()
     check("x0T feat rows max abs / range", (x0T[:256] - feat_t).abs().max().item() / feat_t.abs().max().item(), 4e-3)
     p = pts[0].reshape(S, 3).t()
@@ -59,6 +59,6 @@ def test_stored_activations_match_oracle():
     for li in range(n_stored):
         pre = "neural_rgb.mlp.linears.%d" % li
         h = F.relu(F.linear(h, o_render.wn(sd, pre), sd[pre + ".bias"]))
-        xg = layout.untile(hd["xT"][0, li], 256).float().cpu()
+        xg = layout.unfrag(hd["xT"][0, li], 256).float().cpu()
         check("head0 X%d max abs / range" % (li + 1), (xg - h.t()).abs().max().item() / h.abs().max().item(), 5e-3)
 

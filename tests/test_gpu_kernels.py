@@ -76,6 +76,77 @@ def test_wgrad_wide_jobs_sharing_b(S):
         assert err_w < 1e-4 and err_b < 1e-4
 
 
+@pytest.mark.parametrize("S", [8448, 65536])
+def test_wgrad_operand_layouts_bitwise(S):
+    """Every operand layout mli_wgrad takes (include/mli_hip.h MLI_WGRAD_LAYOUT_*) gives the weight
+    gradient of the feature-major rows call, bit for bit (deterministic mode: fixed-order slice
+    sums), in every launch class: BIG (256 x 256), WIDE (three jobs sharing the 304-row B operand,
+    its last 32-row tile half past the image's 19 k-steps) and THIN (M = 3, a one-k-step A image)
+    -- the tile-blocked images of ABI 14 (the three combinations the engine used) and the fragment
+    images of ABI 15, ACC and NAT order, with a tile stride above rows / 16.  The bias of the
+    fragment kernel is summed from the MFMA A fragments (another fp32 order): within 2e-6 of the
+    rows call, and both within 1e-4 of float64."""
+    _need_gpu()
+    from mli_nerf_amd import _lib as L
+    from mli_nerf_amd import layout
+    g = torch.Generator(device="cpu").manual_seed(11)
+    shared = (torch.randn(304, S, generator=g) * 0.5).half()
+    shapes = [(256, 256, None), (256, 304, shared), (256, 304, shared), (256, 304, shared), (3, 256, None)]
+    ops = []
+    for M, K, b in shapes:
+        a = (torch.randn(M, S, generator=g) * 0.5).half()
+        b = (torch.randn(K, S, generator=g) * 0.5).half() if b is None else b
+        ops.append((a, b))
+
+    def run(kind):
+        keep, jobs, outs = [], [], []
+        dev_b = {}   # one device image per distinct B (the WIDE jobs share one: SHARE_B)
+        for (a, b), (M, K, _) in zip(ops, shapes):
+            dw = torch.zeros(M, K, device=DEV)
+            db = torch.zeros(M, device=DEV)
+            if kind == "rows":
+                A, B, la, lb, ka, kb = a, b, 0, 0, 0, 0
+            elif kind.startswith("tiled"):
+                la, lb = {"tiled11": (1, 1), "tiled01": (0, 1), "tiled10": (1, 0)}[kind]
+                A = layout.to_tiled(a) if la else a
+                B = layout.to_tiled(b) if lb else b
+                ka = kb = 0
+            else:
+                order = kind[5:]
+                ka, kb = (M + 15) // 16 + 1, (K + 15) // 16 + 2   # tile strides above rows / 16
+                A, B = layout.to_frag(a, ka, order), layout.to_frag(b, kb, order)
+                la = lb = L.FRAG_ACC if order == "acc" else L.FRAG_NAT
+            A = A.to(DEV)
+            B = dev_b.setdefault(id(b), B.to(DEV))
+            keep += [A, B, dw, db]
+            jobs.append(L.WgradJob(L.ptr(A), L.ptr(B), M, K, L.ptr(dw), L.ptr(db), K, la, lb, ka, kb))
+            outs.append((dw, db))
+        arr = (L.WgradJob * len(jobs))(*jobs)
+        q = L.WgradArgs(S, len(jobs), C.cast(arr, C.c_void_p), 7, 1, None)
+        ws = torch.empty(max(L.workspace("mli_wgrad", q)[0], 4) // 4, device=DEV)
+        q.workspace = L.ptr(ws)
+        for cls in (1, 2, 4):
+            q.classes = cls
+            L.call("mli_wgrad", q)
+        torch.cuda.synchronize()
+        return [(dw.cpu(), db.cpu()) for dw, db in outs]
+
+    base = run("rows")
+    for i, ((a, b), (dw, db)) in enumerate(zip(ops, base)):
+        rw, rb = a.double() @ b.double().t(), a.double().sum(1)
+        assert ((dw.double() - rw).abs().max() / rw.abs().max()).item() < 1e-4, i
+        assert ((db.double() - rb).abs().max() / rb.abs().max()).item() < 1e-4, i
+    for kind in ("tiled11", "tiled01", "tiled10", "fragacc", "fragnat"):
+        if kind.startswith("tiled") and S % 256:
+            continue
+        for i, ((dw, db), (bw, bb)) in enumerate(zip(run(kind), base)):
+            assert torch.equal(dw, bw), (kind, i, (dw - bw).abs().max().item())
+            if kind.startswith("tiled"):
+                assert torch.equal(db, bb), (kind, i)
+            else:
+                assert ((db - bb).abs().max() / bb.abs().max()).item() < 2e-6, (kind, i)
+
+
 def test_abi_rejects_bad_shapes_and_accepts_empty():
     """Error convention of the C ABI (include/mli_hip.h): shapes a kernel's grid cannot take
     are refused before any launch (non-zero hipError_t -> RuntimeError on the Python side,
@@ -85,9 +156,9 @@ def test_abi_rejects_bad_shapes_and_accepts_empty():
     from mli_nerf_amd.engine import _grid_levels, PathConfig
     # heads forward: R * N must be whole 256-sample workgroups; 1 or 3 heads
     with pytest.raises(RuntimeError, match="mli_rgb_fwd"):
-        L.call("mli_rgb_fwd", L.RgbFwdArgs(3, 32, *([None] * 12), 3))
+        L.call("mli_rgb_fwd", L.RgbFwdArgs(3, 32, *([None] * 11), 3))
     with pytest.raises(RuntimeError, match="mli_rgb_fwd"):
-        L.call("mli_rgb_fwd", L.RgbFwdArgs(8, 32, *([None] * 12), 2))
+        L.call("mli_rgb_fwd", L.RgbFwdArgs(8, 32, *([None] * 11), 2))
     # weight gradients: the sample count must be whole 64-sample k-steps
     with pytest.raises(RuntimeError, match="mli_wgrad"):
         L.call("mli_wgrad", L.WgradArgs(100, 0, None, 7))

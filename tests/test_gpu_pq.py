@@ -81,7 +81,7 @@ def test_pq_output_dw_against_float64():
     N = Nc + 4 * Nf
     S = R * N
     dz4 = eb._bufs["dz4"].view(N, R, 8).permute(1, 0, 2).reshape(S, 8).double()   # tile order m = r*N + k
-    xT = eb._bufs["xT"].view(3, 4, 256 * S)  # tile-blocked [S/256][256][256] per matrix
+    xT = eb._bufs["xT"].view(3, 4, 256 * S)  # ACC fragment images [S/32][16][64][8] per matrix
     sizes = eb._dw_sizes()
     offs, off = [], 0
     for m_, k_ in sizes:
@@ -89,7 +89,7 @@ def test_pq_output_dw_against_float64():
         off += m_ * k_ + m_
     for hdx, (_, _, k_out) in enumerate(layout.HEADS):
         o = offs[hdx * 5 + 4]
-        x3 = layout.untile(xT[hdx, 3], 256).double()             # [256][S]
+        x3 = layout.unfrag(xT[hdx, 3], 256).double()             # [256][S]
         z = dz4[:, 3 * hdx:3 * hdx + k_out]                      # [S][k_out] (scaled)
         ref_w = (z.t() @ x3.t())                                 # [k_out][256]
         ref_b = z.sum(0)

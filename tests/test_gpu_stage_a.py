@@ -160,20 +160,29 @@ def test_stage_a_autograd_path_matches_fused():
     assert _cos(table.grad.cpu(), t_fused.cpu()) > 0.99999
 
 
-def _two_steps_a(world=1, chunk=None, overlap=True, frame=3):
+def _two_steps_a(world=1, chunk=None, overlap=True, frame=3, zero=False):
+    from mli_nerf_amd.trainer import FusedAdamW, ZeroTableAdamW
     cfg, model, trainer, sd, data, u = _setup(32, 16, 4, 100000)
     trainer.world_size = world
     trainer.table_overlap = overlap
     if chunk:
         trainer.table_chunk = chunk
     trainer.model.deterministic = True   # bit-reproducible gradients (fixed-order sums)
+    t = model.neural_sdf.tcnn_encoding.params
+    o = cfg.optim.params
+    if zero:   # the sharded table optimizer (ZeroTableAdamW), else the replicated one
+        import torch.distributed as dist
+        trainer.optim_table = ZeroTableAdamW(t, world, dist.get_rank(), lr=o.lr, weight_decay=o.weight_decay)
+    else:
+        trainer.optim_table = FusedAdamW(t, lr=o.lr, weight_decay=o.weight_decay)
     for s in range(2):
         b = synthetic.make_batch(32, frame=frame + 10 * s)
         trainer.train_step({k: v.to(DEV) for k, v in b.items()}, u=u.to(DEV))
+    trainer.sync_table()
     torch.cuda.synchronize()
-    t = model.neural_sdf.tcnn_encoding.params
+    mv = trainer._table_full_moments if zero else (trainer.optim_table.m, trainer.optim_table.v)
     return dict(table=t.detach().cpu().clone(), table16=model.engine.table16.cpu().clone(),
-                m=trainer.optim_table.m.cpu().clone(), v=trainer.optim_table.v.cpu().clone(),
+                m=mv[0].cpu().clone(), v=mv[1].cpu().clone(),
                 flat=model.flat.detach().cpu().clone(), gtab=trainer._grad_table.cpu().clone())
 
 
@@ -208,6 +217,7 @@ def _world2_worker(rank, port, results):
     try:
         results[(rank, "overlap")] = _two_steps_a(2, chunk=1 << 16, overlap=True, frame=3 + rank)
         results[(rank, "serial")] = _two_steps_a(2, overlap=False, frame=3 + rank)
+        results[(rank, "zero")] = _two_steps_a(2, frame=3 + rank, zero=True)
     finally:
         dist.destroy_process_group()
 
@@ -216,8 +226,9 @@ def _world2_worker(rank, port, results):
 def test_stage_a_world2_on_one_gpu_overlap_equals_serial():
     """Two ranks (gloo, both on cuda:0, different rays) run two stage-a steps with the real HIP
     engine: the overlapped chunked table reduction (chunk i's AdamW behind chunk i's all-reduce)
-    gives the same table, fp16 shadow, moments and MLP buffer as the serial single all-reduce,
-    bit for bit, and the replicas agree."""
+    and the ZeRO-sharded table (reduce-scatter, AdamW on the rank's shard, all-gather of the fp16
+    shadow; the fp32 master and moments gathered by sync_table) give the same table, fp16 shadow,
+    moments and MLP buffer as the serial single all-reduce, bit for bit, and the replicas agree."""
     _need_gpu()
     import socket
     import torch.multiprocessing as mp
@@ -231,4 +242,6 @@ def test_stage_a_world2_on_one_gpu_overlap_equals_serial():
         for k in ("table", "table16", "m", "v", "flat", "gtab"):
             assert torch.equal(results[(r, "overlap")][k], results[(r, "serial")][k]), (r, k)
             assert torch.equal(results[(r, "overlap")][k], results[(0, "overlap")][k]), (r, k)
+            if k != "gtab":   # (the sharded path's gradient buffer holds this rank's own sum)
+                assert torch.equal(results[(r, "zero")][k], results[(r, "serial")][k]), (r, k)
     assert not torch.equal(results[(0, "overlap")]["table"], _two_steps_a(1)["table"])   # the ranks averaged

@@ -23,7 +23,7 @@ sd16 = fp16_table_sd(sd)
 _, feat = o_render.sdf_net(sd16, pcfg, pts, with_feat=True)      # [1,R,N,256]
 feat_t = feat[0].reshape(S, 256).t()                              # [256, S] tile order m = r*N+k
 from mli_nerf_amd import layout  # noqa: E402
-x0T = layout.untile(hd["x0T"], 304).float().cpu()  # tile-blocked image -> [304][S]
+x0T = layout.unfrag(hd["x0T"], 304).float().cpu()  # fragment image -> [304][S]
 e = (x0T[:256] - feat_t).abs()
 print("x0T feat rows: max err %.3e (max |feat| %.3e)" % (e.max(), feat_t.abs().max()))
 p = pts[0].reshape(S, 3).t()
@@ -42,7 +42,7 @@ h = xin
 for li in range(hd["xT"].shape[1]):
     pre = "neural_rgb.mlp.linears.%d" % li
     h = F.relu(F.linear(h, o_render.wn(sd, pre), sd[pre + ".bias"]))
-    xg = layout.untile(hd["xT"][0, li], 256).float().cpu()
+    xg = layout.unfrag(hd["xT"][0, li], 256).float().cpu()
     print("head0 X%d err %.3e (max %.3e)" % (li + 1, (xg - h.t()).abs().max(), h.abs().max()))
 torch.set_printoptions(precision=4, linewidth=200, sci_mode=False)
 print("gpu x0T rows 256..263, samples 0..5:\n", x0T[256:264, :6])
