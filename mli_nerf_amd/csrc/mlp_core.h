@@ -35,7 +35,14 @@ constexpr int X0_KS = MLI_HEAD_K0 / 16;
 constexpr int X0_TILE = X0_KS * FRAG_KS;
 constexpr int Q4_SLOT = 257 * 16;  // one wave's output-layer partials Q in LDS (PQ mode, q4_tile)
 constexpr int DIST = 2;                 // chunks in flight ahead of the one being read (3: no gain)
-constexpr int NSLOT = DIST + 1;
+// Paired phases (run_layer_p): a barrier every second n-tile, the weight ring 4 slots deep.
+// Measured (profiles/r5/pair, alternating on one box): rgb_fwd (train) 1.025 -> 0.929 ms, rgb_bwd
+// 0.737 -> 0.657 ms, step 3.93 -> 3.80 ms against a barrier per n-tile (MLI_HEADS_PAIR=0).
+#ifndef MLI_HEADS_PAIR
+#define MLI_HEADS_PAIR 1
+#endif
+constexpr bool HEADS_PAIR = MLI_HEADS_PAIR;
+constexpr int NSLOT = HEADS_PAIR ? 4 : DIST + 1;
 
 // Wave roles.  ALL: every wave issues its share of the weight DMAs and waits.  Split (DMA +
 // STORE): the first half of the waves (DMA) issue all the LDS-DMA (weights, ReLU masks) and are
@@ -72,10 +79,14 @@ struct Geo {
   static constexpr int LDS_FWD_PQ = PQW_OFF + NW * PQ_WAVE;
   // PQ mode: the first FEAT_KS k-steps of each wave's feat fragments also stay in a wave-private
   // LDS block, so the three heads re-read only the rest from the frag image
-  static constexpr int FEAT_KS = 6;
+  // (even: the feat epilogue writes the two k-steps of a 32-feature tile together; with the
+  // 4-slot ring of HEADS_PAIR only 2 fit beside the PQ blocks)
+  static constexpr int FEAT_KS = HEADS_PAIR ? 2 : 6;
+  static_assert(FEAT_KS % 2 == 0, "whole 32-feature tiles of feat in LDS");
   static constexpr int LDS_FWD_PQF = LDS_FWD_PQ + NW * FEAT_KS * 1024;
   // the eval forward (no PQ blocks): 8 k-steps fit
   static constexpr int FEAT_KS_EVAL = 8;
+  static_assert(FEAT_KS_EVAL % 2 == 0, "whole 32-feature tiles of feat in LDS");
   static constexpr int LDS_FWD_F = LDS_FWD + NW * FEAT_KS_EVAL * 1024;
   // ring DMAs per wave and chunk
   template <int ROLE> static constexpr int ring_ops() { return ROLE == STORE ? 0 : RND; }
@@ -303,6 +314,66 @@ MLI_FI void run_layer_d(Ring& rg, uint8_t* lds, const half8* X, int lane, Bytes&
   }
 }
 
+// run_layer_d in segments of two phases (HEADS_PAIR): the n-tiles of a layer are consumed two per
+// barrier (a layer of one tile is a segment of its own), through a 4-slot ring.  At a segment's
+// start its DMA waves issue the chunks of the NEXT segment (NEXTN of them after the layer's last
+// segment) into the slots the previous segment read; at its end they wait for them -- every VMEM op
+// issued after them is this segment's stores, counted statically -- and the barrier publishes them.
+// A DMA has the same two phases to land as with DIST = 2, while the barriers per layer halve.
+// pre.issue(t) runs at the start of the segment holding phase t, before its chunk DMAs.
+template <class G, int ROLE, int KS, int NT, int EPI, int MASKN, int PREVN, bool DEFER, int NEXTN, class Bytes,
+          class Pre, class Prev, class Epi>
+MLI_FI void run_layer_p(Ring& rg, uint8_t* lds, const half8* X, int lane, Bytes&& bytes, Pre&& pre, Prev&& prev,
+                        Epi&& epi, f32x16& pacc) {
+  static_assert(ROLE != ALL, "split wave roles only");
+  static_assert(NSLOT == 4, "two segments of two chunks in the ring");
+  auto stores = [](int t) MLI_LAMBDA_FI {
+    const int pv = t == 0 ? PREVN : 0;
+    if (DEFER) return pv + (t >= 1 ? EPI : 0);
+    return pv + EPI + (t == NT - 1 ? MASKN : 0);
+  };
+#pragma unroll
+  for (int s = 0; s < NT; s += 2) {
+    const int n_this = NT - s < 2 ? NT - s : 2;
+    const int n_next = s + 2 < NT ? (NT - s - 2 < 2 ? NT - s - 2 : 2) : NEXTN;
+#pragma unroll
+    for (int t = s; t < s + n_this; ++t) pre.issue(t);
+#pragma unroll
+    for (int k = 0; k < n_next; ++k) ring_issue<G, ROLE>(rg, lds, bytes);
+    int n = 0;
+#pragma unroll
+    for (int t = s; t < s + n_this; ++t) {
+      if (t == 0) prev(pacc);
+      const f32x16 acc = chunk_mma<KS, G::PF>(lds + (rg.cur % NSLOT) * G::SLOT, X, lane);
+      if (DEFER) {
+        if (t > 0) epi(t - 1, pacc);
+        pacc = acc;
+      } else {
+        epi(t, acc);
+      }
+      n += stores(t);
+      rg.cur++;
+    }
+    if (ROLE != STORE) vm_wait(n);
+    block_sync();
+  }
+}
+
+// One layer of the heads kernels: run_layer_d (a barrier per n-tile, LASTN) or, with HEADS_PAIR,
+// run_layer_p (NEXTN: the chunks of the segment after this layer).
+template <class G, int ROLE, int KS, int NT, int EPI, int MASKN, int PREVN, bool DEFER, int LASTN, int NEXTN,
+          class Bytes, class Pre, class Prev, class Epi>
+MLI_FI void heads_layer(Ring& rg, uint8_t* lds, const half8* X, int lane, Bytes&& bytes, Pre&& pre, Prev&& prev,
+                        Epi&& epi, f32x16& pacc) {
+  if constexpr (HEADS_PAIR)
+    run_layer_p<G, ROLE, KS, NT, EPI, MASKN, PREVN, DEFER, NEXTN>(rg, lds, X, lane, bytes, pre, prev, epi, pacc);
+  else
+    run_layer_d<G, ROLE, KS, NT, EPI, MASKN, PREVN, DEFER, LASTN>(rg, lds, X, lane, bytes, pre, prev, epi, pacc);
+}
+
+// chunks the heads kernels' prologue issues and waits for before the first barrier
+constexpr int PROLOGUE_CHUNKS = HEADS_PAIR ? 2 : DIST;
+
 // The heads kernels defer every layer's epilogue by one tile.  Measured (profiles/r4/defer2,
 // alternating on one box): step 4.29 / 4.30 -> 4.25 / 4.24 ms, rgb_fwd 1.150 -> 1.108-1.128 ms,
 // rgb_bwd 0.926 -> 0.914-0.920 ms against the same kernels with the epilogue in place; bit-identical.
@@ -489,15 +560,15 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
   // SDF layer 1's output feat (k-steps 0..15 of the tile's x0 image; in training the image is
   // also the WIDE dW operand, with the extras as k-steps 16..18)
   uint16_t* ftile = a.feat_frag + (size_t)tile * X0_TILE;
-  // prologue: chunks 0 .. DIST-1 in flight, wait for chunk 0
+  // prologue: chunks 0 .. DIST-1 in flight, wait for chunk 0 (paired: both first chunks)
 #pragma unroll
-  for (int d = 0; d < DIST; ++d) ring_issue<G, ROLE>(rg, lds, bytes);
+  for (int d = 0; d < PROLOGUE_CHUNKS; ++d) ring_issue<G, ROLE>(rg, lds, bytes);
   if (TRAIN) {
     half8* xd = reinterpret_cast<half8*>(ftile + 16 * FRAG_KS) + lane;
 #pragma unroll
     for (int i = 0; i < 3; ++i) __builtin_nontemporal_store(xe[i], xd + i * 64);
   }
-  if (ROLE != STORE) vm_wait((DIST - 1) * G::template ring_ops<ROLE>() + (TRAIN ? 3 : 0));
+  if (ROLE != STORE) vm_wait((HEADS_PAIR ? 0 : (DIST - 1) * G::template ring_ops<ROLE>()) + (TRAIN ? 3 : 0));
   block_sync();
 
   // SDF layer 1: feat = softplus(W1 h0 + b1) -> A and the x0 image
@@ -523,8 +594,8 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
     }
   };
   // (LASTN: the extras stores follow chunk 1's DMAs)
-  run_layer_d<G, ROLE, 16, 8, 2, 0, 0, HEADS_DEFER, TRAIN ? 3 : 0>(rg, lds, B, lane, bytes, NoPre{}, none, feat_epi,
-                                                                   pacc);
+  heads_layer<G, ROLE, 16, 8, 2, 0, 0, HEADS_DEFER, TRAIN ? 3 : 0, 2>(rg, lds, B, lane, bytes, NoPre{}, none, feat_epi,
+                                                                      pacc);
   if (HEADS_DEFER) feat_epi(7, pacc);  // the last feat tile, before the heads reload feat
 
   for (int hd = 0; hd < a.n_heads; ++hd) {
@@ -574,15 +645,16 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
     constexpr int MN = TRAIN ? 1 : 0, PN = TRAIN && HEADS_DEFER ? 1 : 0;
     constexpr int X = TRAIN ? 2 : 0, X3 = PQ ? 0 : X;
     constexpr int LN = HEADS_DEFER ? X : X + MN;  // stores of a layer's last phase (epi(6) when deferred)
-    run_layer_d<G, ROLE, 19, 8, X, MN, 0, HEADS_DEFER>(rg, lds, B, lane, bytes, NoPre{}, none, e0, pacc);
-    run_layer_d<G, ROLE, 16, 8, X, MN, PN + X, HEADS_DEFER, LN>(rg, lds, A, lane, bytes, NoPre{}, fin(e0), e1, pacc);
-    run_layer_d<G, ROLE, 16, 8, X, MN, PN + X, HEADS_DEFER, LN>(rg, lds, B, lane, bytes, NoPre{}, fin(e1), e2, pacc);
-    run_layer_d<G, ROLE, 16, 8, X3, MN, PN + X, HEADS_DEFER, LN>(rg, lds, A, lane, bytes, NoPre{}, fin(e2), e3, pacc);
+    heads_layer<G, ROLE, 19, 8, X, MN, 0, HEADS_DEFER, 0, 2>(rg, lds, B, lane, bytes, NoPre{}, none, e0, pacc);
+    heads_layer<G, ROLE, 16, 8, X, MN, PN + X, HEADS_DEFER, LN, 2>(rg, lds, A, lane, bytes, NoPre{}, fin(e0), e1, pacc);
+    heads_layer<G, ROLE, 16, 8, X, MN, PN + X, HEADS_DEFER, LN, 2>(rg, lds, B, lane, bytes, NoPre{}, fin(e1), e2, pacc);
+    heads_layer<G, ROLE, 16, 8, X3, MN, PN + X, HEADS_DEFER, LN, 1>(rg, lds, A, lane, bytes, NoPre{}, fin(e2), e3,
+                                                                    pacc);
     const int no = hd == 2 ? 1 : 3;
     const int off = hd * 3;
     float gq[3] = {0.f, 0.f, 0.f};
-    run_layer_d<G, ROLE, 16, 1, 0, 0, PN + X3, false, HEADS_DEFER ? X3 : X3 + MN>(rg, lds, B, lane, bytes, NoPre{},
-                                                                            fin(e3),
+    heads_layer<G, ROLE, 16, 1, 0, 0, PN + X3, false, HEADS_DEFER ? X3 : X3 + MN, 2>(rg, lds, B, lane, bytes, NoPre{},
+                                                                                fin(e3),
                                           [&](int, const f32x16& acc) MLI_LAMBDA_FI {
       if (h == 0) {
 #pragma unroll
@@ -656,8 +728,8 @@ MLI_FI void rgb_bwd_body(const mli_rgb_bwd_args& a, uint8_t* lds) {
   ring_start(rg, a.wbwd, BWD_CHUNKS, bytes);
   mask_dma(0);
 #pragma unroll
-  for (int d = 0; d < DIST; ++d) ring_issue<G, ROLE>(rg, lds, bytes);
-  if (ROLE != STORE) vm_wait((DIST - 1) * G::template ring_ops<ROLE>());
+  for (int d = 0; d < PROLOGUE_CHUNKS; ++d) ring_issue<G, ROLE>(rg, lds, bytes);
+  if (ROLE != STORE) vm_wait(HEADS_PAIR ? 0 : (DIST - 1) * G::template ring_ops<ROLE>());
   block_sync();
 
   half8 A[16], B[16];
@@ -720,10 +792,10 @@ MLI_FI void rgb_bwd_body(const mli_rgb_bwd_args& a, uint8_t* lds) {
     // static store counts: 2 dZ fragments per epilogue (EPI, PREVN and the previous layer's last
     // phase, LASTN)
     constexpr int X = 2, LN = X;
-    run_layer_d<G, ROLE, 1, 8, X, 0, 0, HEADS_DEFER>(rg, lds, &z4, lane, bytes, pre(0), none, e3, pacc);
-    run_layer_d<G, ROLE, 16, 8, X, 0, X, HEADS_DEFER, LN>(rg, lds, A, lane, bytes, pre(1), fin(e3), e2, pacc);
-    run_layer_d<G, ROLE, 16, 8, X, 0, X, HEADS_DEFER, LN>(rg, lds, B, lane, bytes, pre(2), fin(e2), e1, pacc);
-    run_layer_d<G, ROLE, 16, 8, X, 0, X, HEADS_DEFER, LN>(rg, lds, A, lane, bytes, pre(3), fin(e1), e0, pacc);
+    heads_layer<G, ROLE, 1, 8, X, 0, 0, HEADS_DEFER, 0, 2>(rg, lds, &z4, lane, bytes, pre(0), none, e3, pacc);
+    heads_layer<G, ROLE, 16, 8, X, 0, X, HEADS_DEFER, LN, 2>(rg, lds, A, lane, bytes, pre(1), fin(e3), e2, pacc);
+    heads_layer<G, ROLE, 16, 8, X, 0, X, HEADS_DEFER, LN, 2>(rg, lds, B, lane, bytes, pre(2), fin(e2), e1, pacc);
+    heads_layer<G, ROLE, 16, 8, X, 0, X, HEADS_DEFER, LN, 2>(rg, lds, A, lane, bytes, pre(3), fin(e1), e0, pacc);
     if (HEADS_DEFER) e0(7, pacc);  // the head's last tile (its mask slot is not refilled before the
                                    // next head's layer 0 has passed two barriers)
   }

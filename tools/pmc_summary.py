@@ -27,7 +27,9 @@ def short(name):
     table = [("rgb_fwd_kernel", "mli_rgb_fwd"), ("rgb_bwd_kernel", "mli_rgb_bwd"),
              ("dw4_partial_kernel", "mli_dw4"), ("dw4_reduce_kernel", "mli_dw4:reduce"),
              ("wgrad_kernel<256, 256", "mli_wgrad:big"), ("wgrad_dma_kernel<256, 256", "mli_wgrad:big"), ("wgrad_kernel<256, 320", "mli_wgrad:wide"),
-             ("wgrad_kernel<32, 256", "mli_wgrad:thin"), ("wgrad_dma_kernel<256, 320", "mli_wgrad:wide"), ("encode5_kernel", "mli_sdf:field/encode5"),
+             ("wgrad_kernel<32, 256", "mli_wgrad:thin"), ("wgrad_dma_kernel<256, 320", "mli_wgrad:wide"),
+             ("wgrad_frag_kernel<256, 256", "mli_wgrad:big"), ("wgrad_frag_kernel<256, 320", "mli_wgrad:wide"),
+             ("wgrad_frag_kernel<32, 256", "mli_wgrad:thin"), ("encode5_kernel", "mli_sdf:field/encode5"),
              ("field_mlp_kernel", "mli_sdf:field/mlp"), ("sdf_kernel", "mli_sdf:sdf"), ("sample_fine_kernel", "mli_sample_fine"),
              ("composite_fwd_kernel", "mli_composite_fwd"), ("composite_bwd_kernel", "mli_composite_bwd"),
              ("composite_loss_kernel", "mli_composite_loss"), ("composite_loss_finalize", "mli_composite_loss:finalize"),

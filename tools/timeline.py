@@ -4,6 +4,7 @@ import csv
 import sys
 
 SHORT = [("rgb_fwd", "fwd"), ("rgb_bwd", "bwd"), ("wgrad_kernel<256, 256", "BIG"), ("wgrad_dma_kernel<256, 256", "BIG"),
+         ("wgrad_frag_kernel<256, 256", "BIG"), ("wgrad_frag_kernel<256, 320", "WIDE"), ("wgrad_frag_kernel<32", "THIN"),
          ("wgrad_dma", "WIDE"),
          ("wgrad_kernel<32", "THIN"), ("encode5", "enc5"), ("field_mlp", "fmlp"), ("sdf_kernel", "sdf"),
          ("sample_fine", "fine"), ("sample_coarse", "coarse"), ("composite_loss_kernel", "cl"),
