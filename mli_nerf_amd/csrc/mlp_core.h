@@ -73,15 +73,15 @@ struct Geo {
   static constexpr int LDS_BWD = MASK_OFF + 2 * MASKB;
   // PQ mode (rgb_fwd, q4_tile): the waves' Q partials parked for the cross-wave sum, then the
   // per-wave transpose scratch
+  // (HEADS_PAIR: the park is two weight-ring slots free while q4_tile runs, q4_park below)
   static constexpr int QP_OFF = RING;
   static constexpr int PQ_WAVE = 2048 + 256;
-  static constexpr int PQW_OFF = QP_OFF + NW * Q4_SLOT;
+  static constexpr int PQW_OFF = QP_OFF + (HEADS_PAIR ? 0 : NW * Q4_SLOT);
   static constexpr int LDS_FWD_PQ = PQW_OFF + NW * PQ_WAVE;
   // PQ mode: the first FEAT_KS k-steps of each wave's feat fragments also stay in a wave-private
   // LDS block, so the three heads re-read only the rest from the frag image
-  // (even: the feat epilogue writes the two k-steps of a 32-feature tile together; with the
-  // 4-slot ring of HEADS_PAIR only 2 fit beside the PQ blocks)
-  static constexpr int FEAT_KS = HEADS_PAIR ? 2 : 6;
+  // (even: the feat epilogue writes the two k-steps of a 32-feature tile together)
+  static constexpr int FEAT_KS = 6;
   static_assert(FEAT_KS % 2 == 0, "whole 32-feature tiles of feat in LDS");
   static constexpr int LDS_FWD_PQF = LDS_FWD_PQ + NW * FEAT_KS * 1024;
   // the eval forward (no PQ blocks): 8 k-steps fit
@@ -403,11 +403,24 @@ constexpr float Q4_SCALE = MLI_Q4_SCALE;  // g <= 1/4 -> fp16 <= 16384 (undone t
 
 template <class G, int ROLE>
 MLI_FI void q4_tile(const mli_rgb_fwd_args& a, uint8_t* lds, const half8 (&X)[19], const float (&gq)[3], int hd,
-                    int lane) {
+                    int lane, const Ring& rg) {
   const int wave = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
   uint8_t* xr = lds + G::PQW_OFF + wave * G::PQ_WAVE;
   uint8_t* gr = xr + 2048;
-  uint8_t* qs = lds + G::QP_OFF + wave * Q4_SLOT;
+  // the Q park of wave w.  HEADS_PAIR: after the output layer's segment the ring slots of its
+  // chunk (rg.cur - 1) and of the chunk before (rg.cur - 2) are consumed, and the next DMAs into
+  // them go out at the next head's first segment, after q4_tile's last barrier: waves 0..3 park in
+  // the first, 4..7 in the second (4 x 4112 B <= SLOT each)
+  auto q4_park = [&](int w) MLI_LAMBDA_FI {
+    if constexpr (HEADS_PAIR) {
+      static_assert(4 * Q4_SLOT <= G::SLOT && G::NW == 8, "Q park in two ring slots");
+      const int slot = (rg.cur - (w < 4 ? 2 : 1)) % NSLOT;
+      return lds + slot * G::SLOT + (w & 3) * Q4_SLOT;
+    } else {
+      return lds + G::QP_OFF + w * Q4_SLOT;
+    }
+  };
+  uint8_t* qs = q4_park(wave);
   // G^T rows 0..3 (row 3 zero) from the lanes that hold the outputs
   if (h == 0) {
 #pragma unroll
@@ -480,7 +493,7 @@ MLI_FI void q4_tile(const mli_rgb_fwd_args& a, uint8_t* lds, const half8 (&X)[19
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int w = 0; w < G::NW; ++w)
-        if ((t0 + w) * 32 / N - r_first == seg) v += *reinterpret_cast<const f32x4*>(lds + G::QP_OFF + w * Q4_SLOT + row * 16);
+        if ((t0 + w) * 32 / N - r_first == seg) v += *reinterpret_cast<const f32x4*>(q4_park(w) + row * 16);
       __builtin_nontemporal_store(v, qo + ((size_t)seg * a.n_heads + hd) * 257 + row);
     }
   }
@@ -667,7 +680,7 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
       }
     }, pacc);
     // (the q4 stores come from the STORE waves only: the DMA waves' counted waits are unchanged)
-    if (PQ) q4_tile<G, ROLE>(a, lds, B, gq, hd, lane);
+    if (PQ) q4_tile<G, ROLE>(a, lds, B, gq, hd, lane, rg);
   }
   vm_wait(0);  // no LDS-DMA may land after the workgroup's LDS is released
 }
