@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 #include "mli_hip.h"
 
 typedef _Float16 f16;
@@ -20,10 +22,49 @@ typedef __attribute__((address_space(3))) fp16x4_t lds_fp16x4_t;
 // ds_read_b64_tr_b16 (gfx950): a 16-lane group reads a 4-row x 16-column block of 16-bit
 // elements; lane 4q+p of the group supplies the address of row q, columns 4p..4p+3 (8 B),
 // lane i receives column i of the 4 rows (row q in element q).  EXEC must be all ones.
+// (the builtin makes the compiler wait vmcnt(0) before it whenever an LDS-DMA is in flight: it
+// cannot tell the read from the DMA's destination -- fine outside DMA loops; inside them use
+// ds_tr16_at below)
 MLI_FI half4 ds_read_tr16(const void* lds_addr) {
   return __builtin_bit_cast(half4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_fp16x4_t*)lds_addr));
 }
 #define MLI_LAMBDA_FI __attribute__((always_inline))
+
+// 32-bit LDS address of a pointer into the workgroup's LDS
+MLI_FI uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) void*)p);
+}
+// The same transposed read as inline asm, at byte offset OFF from a 32-bit LDS address: the
+// compiler sees no LDS access, so it adds neither the vmcnt(0) wait behind in-flight LDS-DMAs
+// (measured: with the builtin every k-slice stage of mli_wgrad waited for the NEXT stage's
+// DMAs before its first read, so DMA and MFMA never overlapped) nor any lgkmcnt wait for the
+// result: the caller waits with lgkm_wait() and ties the results with tie() before use.
+template <int OFF>
+MLI_FI half4 ds_tr16_at(uint32_t addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
+  half4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
+template <int N>
+MLI_FI void lgkm_wait() {
+  static_assert(N >= 0 && N < 16, "lgkmcnt field");
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(N) : "memory");
+}
+// orders every later use of x behind the asm statements before it (an lgkm_wait)
+template <class T>
+MLI_FI void tie(T& x) {
+  asm volatile("" : "+v"(x));
+}
+// f(std::integral_constant<int, I>) for I = 0 .. N-1, each I a constant expression
+template <class F, int... I>
+MLI_FI void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+MLI_FI void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 // D = A(32x16) * B(16x32) + C on one wave (gfx950 v_mfma_f32_32x32x16_f16).
 // Lane l (r = l & 31, h = l >> 5) holds A[r][k(h,j)] and B[k(h,j)][r] in element j;

@@ -366,12 +366,14 @@ MLI_FI int frag_read_off(int lane, int half, int r, bool nat) {
   return (g & 1) * 1024 + frag_chunk(c, hh, g & 1) * 16 + b8;
 }
 
-template <int BM, int BN, int WM, int WN, int NBUF, bool SHARE_B>
+template <int BM, int BN, int WM, int WN, int NBUF, bool SHARE_B, int TPS>
 __global__ __launch_bounds__(512) void wgrad_frag_kernel(KArgs ka) {
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   constexpr int KA = BM / 16, KB = BN / 16;           // k-steps per tile of each operand's block
-  constexpr int PIECES = 2 * (KA + KB), PPW = (PIECES + 7) / 8;
-  constexpr int STAGE = PIECES * 1024, B_OFF = 2 * KA * 1024;
+  // a stage: TPS 32-sample tiles of both operand blocks
+  constexpr int PIECES = TPS * (KA + KB), PPW = (PIECES + 7) / 8;
+  constexpr int STAGE = PIECES * 1024, B_OFF = TPS * KA * 1024, STG = 32 * TPS;
+  static_assert(64 % STG == 0, "the k-slices are whole stages");
   static_assert(KA % 2 == 0 && KB % 2 == 0, "operand blocks of whole 32-feature tiles");
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   int bid = blockIdx.x;
@@ -396,42 +398,56 @@ __global__ __launch_bounds__(512) void wgrad_frag_kernel(KArgs ka) {
   const int wm = wave / WN, wn = wave - wm * WN;
   const int h = lane >> 5, rl = lane & 31;
 
-  // this lane's DMA sources: piece u * 8 + wave (clamped: a duplicate of the last piece rewrites
-  // the same bytes, so every wave issues PPW per stage and the vmcnt counts are uniform); k-steps
-  // past the operand's last one (rows >= M or K) re-read that k-step, whose rows are discarded
-  const uint16_t* src[PPW];
-  int tstride[PPW];  // halves per 32-sample tile of the piece's image
-  auto piece_of = [&](int u) MLI_LAMBDA_FI { return min(u * 8 + wave, PIECES - 1); };
+  // the DMA sources: piece u * 8 + wave (clamped: a duplicate of the last piece rewrites the
+  // same bytes, so every wave issues PPW per stage and the vmcnt counts are uniform); k-steps
+  // past the operand's last one (rows >= M or K) re-read that k-step, whose rows are discarded.
+  // Per piece a wave-uniform base (SGPRs, the wave index made scalar) plus one of two per-lane
+  // offsets (the chunk swizzle of even / odd k-steps): the DMAs take the saddr form and no
+  // 64-bit address lives in VGPRs (VGPR-held sources spilled once the reads became asm, and the
+  // spill reloads wait vmcnt(0) -- for the DMAs too)
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const uint8_t* sbase[PPW];
+  int tstride[PPW];  // bytes per 32-sample tile of the piece's image
+  int odd[PPW];  // the piece's k-step parity, as the lane offset's swizzle bit (1 << 7)
+  auto piece_of = [&](int u) MLI_LAMBDA_FI { return min(u * 8 + wv, PIECES - 1); };
 #pragma unroll
   for (int u = 0; u < PPW; ++u) {
     const int piece = piece_of(u);
-    const bool in_a = piece < 2 * KA;
-    const int pl = in_a ? piece : piece - 2 * KA, kq = in_a ? KA : KB;
+    const bool in_a = piece < TPS * KA;
+    const int pl = in_a ? piece : piece - TPS * KA, kq = in_a ? KA : KB;
     const int tl = pl / kq, q = pl - tl * kq;
     const int rows = in_a ? J.M : J.K, first = (in_a ? tm * BM : tn * BN) / 16;
     const int kst = in_a ? J.a_kst : J.b_kst;
     const int qg = min(first + q, (rows + 15) / 16 - 1);
-    const int hh = lane >> 5, c = (lane & 31) ^ ((hh << 2) | ((q & 1) << 3));
-    tstride[u] = kst * 512;
-    src[u] = (in_a ? J.a : J.b) + (size_t)tl * tstride[u] + qg * 512 + (32 * hh + c) * 8;
+    tstride[u] = kst * 1024;
+    sbase[u] = reinterpret_cast<const uint8_t*>(in_a ? J.a : J.b) + (size_t)tl * tstride[u] + qg * 1024;
+    odd[u] = (q & 1) << 7;
   }
+  // lane (c, hh) of an even k-step's piece: 16 B at (32 hh + (c ^ 4 hh)) * 16; odd: c ^ 8 as well
+  const uint32_t voff = (32 * (lane >> 5) + ((lane & 31) ^ ((lane >> 5) << 2))) * 16;
   auto issue = [&](int s, int buf) MLI_LAMBDA_FI {
-    const int kk = min(k0 + s * 64, k1 - 64);  // past the end: a dummy refetch, never consumed
+    const int kk = min(k0 + s * STG, k1 - STG);  // past the end: a dummy refetch, never consumed
 #pragma unroll
     for (int u = 0; u < PPW; ++u) {
-      glds16(src[u] + (size_t)(kk >> 5) * tstride[u], lds + buf * STAGE + piece_of(u) * 1024);
+      const uint8_t* sp = sbase[u] + (size_t)(kk >> 5) * tstride[u];
+      glds16(sp + (voff ^ (uint32_t)odd[u]), lds + buf * STAGE + piece_of(u) * 1024);
     }
   };
-  // transposed-read offsets (order per operand) for the 2 x 2 (MFMA k-step half, read) combinations
+  // 32-bit LDS addresses (stage buffer 0) of this lane's transposed reads of its wave's operand
+  // blocks, per (MFMA k-step half, read) combination; the block and tile offsets inside a stage
+  // are the reads' immediate offsets
   const bool a_nat = J.a_tiled == 3, b_nat = J.b_tiled == 3;
-  int offa[2][2], offb[2][2];
+  uint32_t ba[2][2], bb[2][2];
+  {
+    const uint32_t l0 = lds_addr(lds);
 #pragma unroll
-  for (int hf = 0; hf < 2; ++hf)
+    for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      offa[hf][r] = frag_read_off(lane, hf, r, a_nat);
-      offb[hf][r] = B_OFF + frag_read_off(lane, hf, r, b_nat);
-    }
+      for (int r = 0; r < 2; ++r) {
+        ba[hf][r] = l0 + 2 * wm * TM * 1024 + frag_read_off(lane, hf, r, a_nat);
+        bb[hf][r] = l0 + B_OFF + 2 * wn * TN * 1024 + frag_read_off(lane, hf, r, b_nat);
+      }
+  }
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -448,44 +464,54 @@ __global__ __launch_bounds__(512) void wgrad_frag_kernel(KArgs ka) {
   for (int i = 0; i < TM; ++i) bsum[i] = 0.f;
   const half2 ones = {(f16)1.f, (f16)1.f};
 
-  const int n_st = (k1 - k0) / 64;
+  const int n_st = (k1 - k0) / STG;
 #pragma unroll
   for (int d = 0; d < NBUF - 1; ++d) issue(d, d);
   for (int st = 0; st < n_st; ++st) {
     vm_wait((NBUF - 2) * PPW);  // this wave's DMAs of stage st have landed
     block_sync();               // ... every wave's; and everyone is done with stage st - 1
     issue(st + NBUF - 1, (st + NBUF - 1) % NBUF);
-    const uint8_t* sb = lds + (st % NBUF) * STAGE;
-    // the 4 MFMA k-steps of the stage, each one's operand fragments read during the previous
-    // one's MFMAs (double-buffered registers: the transposed reads are twice the instructions of
-    // plain b128 reads, measured 0.83 against 0.89 ms for BIG with their latency exposed)
-    half8 fa[2][TM], fb[2][TN];
-    auto read = [&](int ks, half8 (&ra)[TM], half8 (&rb)[TN]) MLI_LAMBDA_FI {
-      const int tl = ks >> 1, hf = ks & 1;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const uint8_t* blk = sb + (tl * KA + 2 * (wm * TM + i)) * 1024;
-        const half4 lo = ds_read_tr16(blk + offa[hf][0]), hi = ds_read_tr16(blk + offa[hf][1]);
-        ra[i] = half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const uint8_t* blk = sb + (tl * KB + 2 * (wn * TN + j)) * 1024;
-        const half4 lo = ds_read_tr16(blk + offb[hf][0]), hi = ds_read_tr16(blk + offb[hf][1]);
-        rb[j] = half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
+    const uint32_t so = (st % NBUF) * STAGE;
+    // The 2 TPS MFMA k-steps of the stage.  A fragments double-buffered: k-step ks + 1's go out
+    // at the start of k-step ks.  B fragments single-buffered, refilled progressively: the MFMAs
+    // run column block by column block (j), and B fragment j of k-step ks + 1 is read into the
+    // registers of k-step ks's the moment its last MFMA has issued -- about TN MFMA pairs of
+    // cover, 20 VGPRs fewer than double-buffering B (WIDE sits at the 256-register limit of two
+    // waves per SIMD).  The reads are asm (ds_tr16_at): the counted waits below are exact.
+    auto read_a = [&](auto KSc, half8 (&ra)[TM]) MLI_LAMBDA_FI {
+      constexpr int ks = decltype(KSc)::value, tl = ks >> 1, hf = ks & 1;
+      static_for<TM>([&](auto Ic) MLI_LAMBDA_FI {
+        constexpr int o = (tl * KA + 2 * decltype(Ic)::value) * 1024;
+        const half4 lo = ds_tr16_at<o>(ba[hf][0] + so), hi = ds_tr16_at<o>(ba[hf][1] + so);
+        ra[decltype(Ic)::value] = half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      });
     };
-    read(0, fa[0], fb[0]);
+    auto read_b = [&](auto KSc, auto Jc, half8& rb) MLI_LAMBDA_FI {
+      constexpr int ks = decltype(KSc)::value, tl = ks >> 1, hf = ks & 1;
+      constexpr int o = (tl * KB + 2 * decltype(Jc)::value) * 1024;
+      const half4 lo = ds_tr16_at<o>(bb[hf][0] + so), hi = ds_tr16_at<o>(bb[hf][1] + so);
+      rb = half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    };
+    half8 fa[2][TM], fb[TN];
+    read_a(std::integral_constant<int, 0>{}, fa[0]);
+    static_for<TN>([&](auto Jc) MLI_LAMBDA_FI { read_b(std::integral_constant<int, 0>{}, Jc, fb[decltype(Jc)::value]); });
+    static_for<2 * TPS>([&](auto KSc) MLI_LAMBDA_FI {
+      constexpr int ks = decltype(KSc)::value, cb = ks & 1;
+      constexpr bool next = ks + 1 < 2 * TPS;
+      if constexpr (next) read_a(std::integral_constant<int, ks + 1>{}, fa[cb ^ 1]);
+      static_for<TN>([&](auto Jc) MLI_LAMBDA_FI {
+        constexpr int j = decltype(Jc)::value;
+        // issued after B(ks)[j]: B(ks)[j+1 ..], A(ks+1), B(ks+1)[0 .. j-1] -- 2 reads each
+        lgkm_wait<next ? 2 * (TN - 1 + TM) : 2 * (TN - 1 - j)>();
+        if constexpr (j == 0) {
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int cb = ks & 1;
-#ifndef MLI_XP_NOPIPE
-      if (ks < 3) read(ks + 1, fa[cb ^ 1], fb[cb ^ 1]);
-#endif
+          for (int i = 0; i < TM; ++i) tie(fa[cb][i]);
+        }
+        tie(fb[j]);
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32(fa[cb][i], fb[cb][j], acc[i][j]);
+        for (int i = 0; i < TM; ++i) acc[i][j] = mfma32(fa[cb][i], fb[j], acc[i][j]);
+        if constexpr (next) read_b(std::integral_constant<int, ks + 1>{}, Jc, fb[j]);
+      });
       if (do_bias) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -493,10 +519,7 @@ __global__ __launch_bounds__(512) void wgrad_frag_kernel(KArgs ka) {
           for (int e = 0; e < 8; e += 2)
             bsum[i] = __builtin_amdgcn_fdot2(half2{fa[cb][i][e], fa[cb][i][e + 1]}, ones, bsum[i], false);
       }
-#ifdef MLI_XP_NOPIPE
-      if (ks < 3) read(ks + 1, fa[cb ^ 1], fb[cb ^ 1]);
-#endif
-    }
+    });
   }
   vm_wait(0);  // the dummy refetches land before the workgroup's LDS is released
   float* slab = nullptr;
@@ -666,8 +689,14 @@ constexpr int WIDE_DMA = 2, WIDE_BKD = 64;
 // BIG through the same ring, 2 stages of 64 samples: 0.898 -> 0.847 ms (register staging of 64
 // samples before; the ring at 32-sample stages -- 64 B row segments -- measured 0.998 ms)
 constexpr int BIG_DMA = 2;
-// the fragment-image kernel (every class): 2 stages of 64 samples (BIG: 2 x 64 KiB)
-constexpr int FRAG_NBUF = 2;
+// the fragment-image kernel (every class): FRAG_NBUF stages of FRAG_TPS 32-sample tiles
+#ifndef MLI_FRAG_TPS
+#define MLI_FRAG_TPS 2
+#endif
+#ifndef MLI_FRAG_NBUF
+#define MLI_FRAG_NBUF 2
+#endif
+constexpr int FRAG_TPS = MLI_FRAG_TPS, FRAG_NBUF = MLI_FRAG_NBUF;
 
 inline int job_class(const mli_wgrad_job& j) {
   return j.M <= 32 ? CLS_THIN : (j.K <= 256 ? CLS_BIG : CLS_WIDE);
@@ -746,13 +775,15 @@ int launch(const mli_wgrad_args* a, int cls, bool frag, hipStream_t s) {
   int grid = 0;
   for (int i = 0; i < ka.n_jobs; ++i) grid += ((ka.jobs[i].M + BM - 1) / BM) * ka.jobs[i].tiles_n * ka.n_split;
   if (frag) {
-    // fragment images: the LDS-DMA ring of 64-sample stages, FRAG_NBUF stages
-    constexpr int LDS = FRAG_NBUF * 2 * (BM / 16 + BN / 16) * 1024;
+    // fragment images: the LDS-DMA ring, FRAG_NBUF stages of FRAG_TPS tiles
+    constexpr int LDS = FRAG_NBUF * FRAG_TPS * (BM / 16 + BN / 16) * 1024;
+    static_assert(LDS <= 160 * 1024, "LDS");
     if (SHARE_B && ka.share)
-      hipLaunchKernelGGL((wgrad_frag_kernel<BM, BN, WM, WN, FRAG_NBUF, SHARE_B>),
+      hipLaunchKernelGGL((wgrad_frag_kernel<BM, BN, WM, WN, FRAG_NBUF, SHARE_B, FRAG_TPS>),
                          dim3(8 * ka.n_jobs * ((ka.n_split + 7) / 8)), dim3(512), LDS, s, ka);
     else
-      hipLaunchKernelGGL((wgrad_frag_kernel<BM, BN, WM, WN, FRAG_NBUF, false>), dim3(grid), dim3(512), LDS, s, ka);
+      hipLaunchKernelGGL((wgrad_frag_kernel<BM, BN, WM, WN, FRAG_NBUF, false, FRAG_TPS>), dim3(grid), dim3(512), LDS,
+                         s, ka);
   } else if (SHARE_B && ka.share) {
     grid = 8 * ka.n_jobs * ((ka.n_split + 7) / 8);
     if constexpr (SHARE_B && DMA_NBUF > 0)
