@@ -32,7 +32,8 @@
  *     NAT order: 16 q + 8 h + j                        (the hash-grid encodings)
  *     ACC order: 16 q + 8 (j >> 2) + 4 h + (j & 3)    (an MFMA accumulator tile's registers:
  *                h0, feat, and every training activation / gradient image the weight
- *                gradients read -- x0 (= feat_frag), xT, dzT, dz4T, dz1T; ABI 15)
+ *                gradients read -- x0 (= feat_frag), xT, dzT, dz4T, dz1T; ABI 15;
+ *                stage a's dZ0 of the SDF layer 0, ABI 16)
  *   feature-major: [features][S] fp16 rows (S contiguous), in tile order m.
  *   tile-blocked (ABI 14): [S/256][features][256] fp16 -- the 256 samples of one workgroup
  *   of every feature row contiguous (still accepted by mli_wgrad).
@@ -51,7 +52,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mli_stream_t; /* == hipStream_t */
 
-#define MLI_ABI_VERSION 15
+#define MLI_ABI_VERSION 16
 #define MLI_HIDDEN 256
 #define MLI_LEVELS 16
 #define MLI_LEVEL_FEAT 8
@@ -283,6 +284,10 @@ typedef struct {
                              k-steps -- the layout mli_rgb_fwd / mli_rgb_bwd / mli_geo_bwd write
                              (ABI 15).  A job's two operands are both frag images or neither.    */
   int a_kst, b_kst;       /* frag images: k-steps per 32-sample tile (>= ceil(rows / 16)); else 0 */
+  const uint16_t* b2_rows; /* frag images only, or NULL: B's k-steps b2_q .. come from this second
+                              frag image (b2_kst k-steps per tile, B's order and tile count) -- the
+                              SDF layer-0 input [enc 128 | p 3] of mli_sdf_bwd (ABI 16)            */
+  int b2_q, b2_kst;
 } mli_wgrad_job;
 #define MLI_WGRAD_LAYOUT_ROWS 0
 #define MLI_WGRAD_LAYOUT_TILED 1
@@ -378,8 +383,9 @@ int mli_geo_bwd_workspace(const mli_geo_bwd_args* a, int64_t* bytes);
 /* SDF layer 0 + sdf head backward for the 5 points of every sample (center + 4 taps):
  * combines d sdf / d grad (composite), eikonal / curvature gradients, the normalize
  * backward of d normal and the tap stencils into d sdf_i; recomputes layer 0 of every point
- * from the FIELD encodings; writes d enc (fp32, for mli_hash_bwd), dZ0 frag images and the
- * p rows of the layer-0 input (for the dW GEMM) and dW/db of linear_sdf (per-wave sums in
+ * from the FIELD encodings; writes d enc (fp32, for mli_hash_bwd), the dZ0 and p fragment
+ * images of the layer-0 weight gradient (ABI 16: mli_wgrad reads them beside the FIELD
+ * encodings, no row conversion) and dW/db of linear_sdf (per-wave sums in
  * LDS, per-workgroup partials in `partials`, summed in workgroup order by a second launch). */
 typedef struct {
   int R, N;
@@ -396,8 +402,11 @@ typedef struct {
   float w_eikonal, w_curvature;  /* loss weights / (R*N) are applied in-kernel */
   float grad_scale;
   float* d_enc;           /* [S/32][5][8][64][8] fp32 (unscaled) */
-  uint16_t* dz0_rows;     /* [256][5S] fp16 scaled dZ0 of the 5 points, column pi*S + m (wgrad rows) */
-  uint16_t* x0_rows;      /* [131][5S] fp16 layer-0 input rows (p 0..2, enc 3..130); this writes rows 0..2 */
+  uint16_t* dz0_frag;     /* [S/32][5][16][64][8] fp16 ACC frag image of the scaled dZ0 of the 5 points:
+                             5S samples in the enc image's order (32-sample tile t of point pi is
+                             image tile 5 t + pi)                                               */
+  uint16_t* p_frag;       /* [S/32][5][1][64][8] fp16 NAT frag image of the points p (features
+                             0..2, rest 0), the same tile order: the layer-0 input's last k-step  */
   float* dw_sdf;          /* [256] scaled (written) */
   float* db_sdf;          /* [1] scaled (written) */
   const float* d_grad_ext; /* optional [N][R][3] d loss / d gradients from outside (autograd) */
@@ -405,7 +414,7 @@ typedef struct {
   float* partials;        /* scratch [workgroups][257] */
 } mli_sdf_bwd_args;
 int mli_sdf_bwd(const mli_sdf_bwd_args* a, mli_stream_t s);
-/* bytes[0..3]: d_enc, dz0_rows, x0_rows, partials. */
+/* bytes[0..3]: d_enc, dz0_frag, p_frag, partials. */
 int mli_sdf_bwd_workspace(const mli_sdf_bwd_args* a, int64_t* bytes);
 
 /* W0_enc^T fragments (A operand of d enc = W0_enc^T dZ0; rows ordered so each lane half

@@ -74,16 +74,19 @@ class RgbBwdArgs(C.Structure):
 
 class WgradJob(C.Structure):
     _fields_ = [("a_rows", P), ("b_rows", P), ("M", I32), ("K", I32), ("dw", P), ("db", P), ("ldw", I32),
-                ("a_tiled", I32), ("b_tiled", I32), ("a_kst", I32), ("b_kst", I32)]
+                ("a_tiled", I32), ("b_tiled", I32), ("a_kst", I32), ("b_kst", I32), ("b2_rows", P),
+                ("b2_q", I32), ("b2_kst", I32)]
 
 
 # mli_wgrad_job operand layouts (MLI_WGRAD_LAYOUT_*)
 ROWS, TILED, FRAG_ACC, FRAG_NAT = 0, 1, 2, 3
 
 
-def frag_job(a, b, M, K, dw, db, ldw, a_kst, b_kst, order=FRAG_ACC):
-    """A mli_wgrad job over two fragment images (ABI 15) with a_kst / b_kst k-steps per tile."""
-    return WgradJob(a, b, M, K, dw, db, ldw, order, order, a_kst, b_kst)
+def frag_job(a, b, M, K, dw, db, ldw, a_kst, b_kst, order=FRAG_ACC, b_order=None, b2=None, b2_q=0, b2_kst=0):
+    """A mli_wgrad job over two fragment images (ABI 15) with a_kst / b_kst k-steps per tile;
+    b2: B's k-steps from b2_q on come from a second image with b2_kst k-steps per tile (ABI 16)."""
+    return WgradJob(a, b, M, K, dw, db, ldw, order, order if b_order is None else b_order, a_kst, b_kst,
+                    b2, b2_q, b2_kst)
 
 
 class WgradArgs(C.Structure):
@@ -162,8 +165,8 @@ class SdfBwdArgs(C.Structure):
     _fields_ = [("R", I32), ("N", I32), ("center", P), ("ray_unit", P), ("dists", P), ("outside", P),
                 ("grad", P), ("hess", P), ("d_sdf", P), ("d_grad", P), ("d_nrm", P), ("dh0_frag", P), ("enc", P),
                 ("wsdf", P), ("wsdf_t", P), ("eps", F32), ("grad_den", F32), ("hess_den", F32),
-                ("w_eikonal", F32), ("w_curvature", F32), ("grad_scale", F32), ("d_enc", P), ("dz0_rows", P),
-                ("x0_rows", P), ("dw_sdf", P), ("db_sdf", P), ("d_grad_ext", P), ("d_hess_ext", P),
+                ("w_eikonal", F32), ("w_curvature", F32), ("grad_scale", F32), ("d_enc", P), ("dz0_frag", P),
+                ("p_frag", P), ("dw_sdf", P), ("db_sdf", P), ("d_grad_ext", P), ("d_hess_ext", P),
                 ("partials", P)]
 
 
@@ -197,7 +200,7 @@ class FragRowsArgs(C.Structure):
                 ("ld", I64), ("col0", I64), ("row0", I32)]
 
 
-ABI_VERSION = 15  # include/mli_hip.h MLI_ABI_VERSION
+ABI_VERSION = 16  # include/mli_hip.h MLI_ABI_VERSION
 
 ENTRY_POINTS = {
     "mli_rays": RaysArgs, "mli_hashgrid_fwd": HashgridArgs, "mli_sdf": SdfArgs,

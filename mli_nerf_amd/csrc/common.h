@@ -46,6 +46,47 @@ MLI_FI half4 ds_tr16_at(uint32_t addr) {
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
   return r;
 }
+// A 16 B global load as inline asm.  Loads, stores and LDS-DMAs of a wave retire in issue order
+// (MI355X_MICROARCH.md, vmcnt), but the compiler treats a counter with loads AND stores pending
+// as out of order and waits vmcnt(0) for any load result -- draining the weight DMAs and the
+// activation stores in flight.  The caller waits with a counted vm_wait() (common.h) and tie()s
+// the result; the memory clobber keeps the compiler's own VMEM ops on their side of it, so the
+// counts stay exact.
+MLI_FI half8 gload16(const void* p) {
+  half8 r;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+
+// Global stores as inline asm (the heads / geometry kernels): with no store visible to it, the
+// compiler counts the loads and LDS-DMAs it waits for as in order and waits exactly, instead of
+// vmcnt(0) (see gload16).  No memory clobber: they may move among the compiler's own memory ops
+// inside a phase, never across the volatile vm_wait / block_sync asm -- all the counted waits
+// need.  (A later load of the same address by the same wave is ordered by the hardware.)
+// (the s_nop 1: a VALU write of the data registers right after a dwordx4 store would change what
+// it stores; hipcc pads its own stores, not asm ones -- the first build without it stored
+// address bits into the x0 image)
+MLI_FI void gstore_nt(void* p, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(p), "v"(v));
+}
+MLI_FI void gstore_nt(void* p, half8 v) { gstore_nt(p, __builtin_bit_cast(u32x4, v)); }
+MLI_FI void gstore_nt(void* p, f32x4 v) { gstore_nt(p, __builtin_bit_cast(u32x4, v)); }
+MLI_FI void gstore(void* p, half8 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(__builtin_bit_cast(u32x4, v)));
+}
+MLI_FI void gstore_f32(void* p, float v) { asm volatile("global_store_dword %0, %1, off" ::"v"(p), "v"(v)); }
+
+// LDS writes as inline asm: a compiler-visible LDS write while an LDS-DMA may be in flight is
+// preceded by vmcnt(0) (the compiler cannot tell it from the DMA's destination).  The caller
+// orders them against plain LDS accesses with asm("" ::: "memory") fences (LDS operations of a
+// wave execute in order, so no wait is needed between a write and a later read of it).
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+MLI_FI void ds_write_u16(uint32_t addr, uint32_t v) { asm volatile("ds_write_b16 %0, %1" ::"v"(addr), "v"(v)); }
+MLI_FI void ds_write_u64(uint32_t addr, u32x2 v) { asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(v)); }
+MLI_FI void ds_write_f128(uint32_t addr, f32x4 v) {
+  asm volatile("ds_write_b128 %0, %1\n\ts_nop 1" ::"v"(addr), "v"(v));
+}
+
 template <int N>
 MLI_FI void lgkm_wait() {
   static_assert(N >= 0 && N < 16, "lgkmcnt field");
@@ -216,6 +257,8 @@ MLI_FI void vm_wait(int n) {
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
+// vm_wait for a wave-uniform count known only at run time (a scalar branch tree)
+MLI_FI void vm_wait_rt(int n) { vm_wait(__builtin_amdgcn_readfirstlane(n)); }
 
 // LDS writes visible to the workgroup; no vector-memory drain (raw barrier: __syncthreads'
 // fence would wait for every outstanding DMA and store)

@@ -163,8 +163,8 @@ MLI_FI void frag_store2(uint16_t* tile_img, int t, half8 f0, half8 f1, int lane)
   half8* d = reinterpret_cast<half8*>(tile_img) + (2 * t) * 64 + lane;
   // streaming (non-temporal) stores: the activations are re-read only by a later kernel, so
   // they should not evict the weight chunks every phase re-reads from L2
-  __builtin_nontemporal_store(f0, d);
-  __builtin_nontemporal_store(f1, d + 64);
+  gstore_nt(d, f0);
+  gstore_nt(d + 64, f1);
 }
 
 // ReLU as one v_max_i32 on the bit pattern: fmaxf on an MFMA result adds a canonicalising
@@ -403,7 +403,7 @@ constexpr float Q4_SCALE = MLI_Q4_SCALE;  // g <= 1/4 -> fp16 <= 16384 (undone t
 
 template <class G, int ROLE>
 MLI_FI void q4_tile(const mli_rgb_fwd_args& a, uint8_t* lds, const half8 (&X)[19], const float (&gq)[3], int hd,
-                    int lane, const Ring& rg) {
+                   int lane, const Ring& rg) {
   const int wave = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
   uint8_t* xr = lds + G::PQW_OFF + wave * G::PQ_WAVE;
   uint8_t* gr = xr + 2048;
@@ -421,10 +421,13 @@ MLI_FI void q4_tile(const mli_rgb_fwd_args& a, uint8_t* lds, const half8 (&X)[19
     }
   };
   uint8_t* qs = q4_park(wave);
+  // (every LDS write and transposed read of q4_tile is asm: compiler-visible ones were preceded by
+  // vmcnt(0) -- the next head's first weight DMAs are in flight -- draining the wave's stores)
   // G^T rows 0..3 (row 3 zero) from the lanes that hold the outputs
   if (h == 0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<f16*>(gr + i * 64 + c * 2) = (f16)(i < 3 ? gq[i] : 0.f);
+    for (int i = 0; i < 4; ++i)
+      ds_write_u16(lds_addr(gr + i * 64 + c * 2), __builtin_bit_cast(uint16_t, (f16)(i < 3 ? gq[i] : 0.f)));
   }
   asm volatile("" ::: "memory");
   half8 gf[2];
@@ -447,26 +450,26 @@ MLI_FI void q4_tile(const mli_rgb_fwd_args& a, uint8_t* lds, const half8 (&X)[19
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
         const int ch = (4 * u + 2 * jj + h) ^ ((c >> 1) & 7);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(xr + c * 64 + ch * 8);
-        *reinterpret_cast<uint2*>(dst) = make_uint2(w[2 * jj], w[2 * jj + 1]);
+        ds_write_u64(lds_addr(xr + c * 64 + ch * 8), u32x2{w[2 * jj], w[2 * jj + 1]});
       }
     }
-    asm volatile("" ::: "memory");
     f32x16 acc;
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    half8 xf[2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int s0 = 16 * ks + 8 * h + q, s1 = s0 + 4;
-      const half4 lo = ds_read_tr16(xr + s0 * 64 + (chunk ^ ((s0 >> 1) & 7)) * 8);
-      const half4 hi = ds_read_tr16(xr + s1 * 64 + (chunk ^ ((s1 >> 1) & 7)) * 8);
-      half8 xf;
-      xf[0] = lo[0]; xf[1] = lo[1]; xf[2] = lo[2]; xf[3] = lo[3];
-      xf[4] = hi[0]; xf[5] = hi[1]; xf[6] = hi[2]; xf[7] = hi[3];
-      acc = mfma32(gf[ks], xf, acc);
+      const half4 lo = ds_tr16_at<0>(lds_addr(xr + s0 * 64 + (chunk ^ ((s0 >> 1) & 7)) * 8));
+      const half4 hi = ds_tr16_at<0>(lds_addr(xr + s1 * 64 + (chunk ^ ((s1 >> 1) & 7)) * 8));
+      xf[ks] = half8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     }
-    asm volatile("" ::: "memory");  // the next block's writes stay behind these reads
-    if (h == 0) *reinterpret_cast<f32x4*>(qs + (32 * b + c) * 16) = f32x4{acc[0], acc[1], acc[2], acc[3]};
+    lgkm_wait<0>();
+    tie(xf[0]);
+    tie(xf[1]);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) acc = mfma32(gf[ks], xf[ks], acc);
+    if (h == 0) ds_write_f128(lds_addr(qs + (32 * b + c) * 16), f32x4{acc[0], acc[1], acc[2], acc[3]});
   }
   // bias row 256: sum_s g_sc (fp32)
   float sb[3];
@@ -477,7 +480,7 @@ MLI_FI void q4_tile(const mli_rgb_fwd_args& a, uint8_t* lds, const half8 (&X)[19
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     sb[i] = v;
   }
-  if (lane == 0) *reinterpret_cast<f32x4*>(qs + 256 * 16) = f32x4{sb[0], sb[1], sb[2], 0.f};
+  if (lane == 0) ds_write_f128(lds_addr(qs + 256 * 16), f32x4{sb[0], sb[1], sb[2], 0.f});
   block_sync();
   if (ROLE != DMA) {
     // ray segments of the workgroup: tile t holds ray 32 t / N
@@ -494,7 +497,7 @@ MLI_FI void q4_tile(const mli_rgb_fwd_args& a, uint8_t* lds, const half8 (&X)[19
 #pragma unroll
       for (int w = 0; w < G::NW; ++w)
         if ((t0 + w) * 32 / N - r_first == seg) v += *reinterpret_cast<const f32x4*>(q4_park(w) + row * 16);
-      __builtin_nontemporal_store(v, qo + ((size_t)seg * a.n_heads + hd) * 257 + row);
+      gstore_nt(qo + ((size_t)seg * a.n_heads + hd) * 257 + row, v);
     }
   }
   block_sync();  // the Q park is free again
@@ -525,11 +528,13 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
   ring_start(rg, a.wfwd, 8 + a.n_heads * 33, bytes);
 
   half8 A[16], B[19];
-  // h0 frags (SDF layer-0 activations) -> B[0..15]
+  // h0 frags (SDF layer-0 activations) -> B[0..15] (asm loads, waited after the prologue: see
+  // gload16 -- with the extras stores pending the compiler waited vmcnt(0) for them inside the
+  // feat layer, draining its first weight DMAs)
   {
     const half8* src = reinterpret_cast<const half8*>(a.h0 + (size_t)tile * FRAG_TILE) + lane;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) B[q] = src[q * 64];
+    for (int q = 0; q < 16; ++q) B[q] = gload16(src + q * 64);
   }
   // extras (NAT order): k-step 16 = [p, n, 0...], 17 = SH(light), 18 = SH(view); in training
   // also as k-steps 16..18 of the x0 image, in ACC order (xe, stored after the prologue DMAs)
@@ -579,9 +584,13 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
   if (TRAIN) {
     half8* xd = reinterpret_cast<half8*>(ftile + 16 * FRAG_KS) + lane;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) __builtin_nontemporal_store(xe[i], xd + i * 64);
+    for (int i = 0; i < 3; ++i) gstore_nt(xd + i * 64, xe[i]);
   }
-  if (ROLE != STORE) vm_wait((HEADS_PAIR ? 0 : (DIST - 1) * G::template ring_ops<ROLE>()) + (TRAIN ? 3 : 0));
+  // (the h0 loads are older than the prologue DMAs and the extras stores: STORE waves, which
+  // issue no DMAs, wait for them here too)
+  vm_wait((HEADS_PAIR || ROLE == STORE ? 0 : (DIST - 1) * G::template ring_ops<ROLE>()) + (TRAIN ? 3 : 0));
+#pragma unroll
+  for (int q = 0; q < 16; ++q) tie(B[q]);
   block_sync();
 
   // SDF layer 1: feat = softplus(W1 h0 + b1) -> A and the x0 image
@@ -598,8 +607,8 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
     A[2 * t] = acc_to_frag(v, 0);
     A[2 * t + 1] = acc_to_frag(v, 1);
     half8* dst = reinterpret_cast<half8*>(ftile) + (2 * t) * 64 + lane;
-    dst[0] = A[2 * t];
-    dst[64] = A[2 * t + 1];
+    gstore(dst, A[2 * t]);
+    gstore(dst + 64, A[2 * t + 1]);
     if (2 * t + 1 < FKS) {  // (the image keeps every k-step: the vmcnt counts are static)
       half8* fl = reinterpret_cast<half8*>(lds + FOFF + wave * FKS * 1024) + (2 * t) * 64 + lane;
       fl[0] = A[2 * t];
@@ -611,16 +620,32 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
                                                                       pacc);
   if (HEADS_DEFER) feat_epi(7, pacc);  // the last feat tile, before the heads reload feat
 
+  // feat into B[0..15] for each head (B[16..18] keep the extras).  Head 0: the feat layer's
+  // output, still in A.  Heads 1, 2: k-steps < FKS from the wave's LDS block, the rest reloaded
+  // from the frag image by asm loads (gload16), waited for by layer 0 after its first weight DMAs
+  // went out (l0_wait): compiler-visible loads were waited with vmcnt(0), draining those DMAs.
+  // The lane offset is made opaque per head so the addresses are not hoisted out of the head
+  // loop (spills).
   for (int hd = 0; hd < a.n_heads; ++hd) {
     const int S = opaque_s(a.R * a.N);
-    // reload feat frags into B[0..15] (B[16..18] keep the extras); the lane offset is made
-    // opaque per head so the 16 addresses are not hoisted out of the head loop (spills)
-    {
+    if (hd == 0) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) B[q] = A[q];
+    } else {
       const half8* src = reinterpret_cast<const half8*>(ftile) + opaque_v(lane);
       const half8* fl = reinterpret_cast<const half8*>(lds + FOFF + wave * (FKS > 0 ? FKS : 1) * 1024) + lane;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) B[q] = q < FKS ? fl[q * 64] : src[q * 64];
+      for (int q = 0; q < 16; ++q) B[q] = q < FKS ? fl[q * 64] : gload16(src + q * 64);
     }
+    // layer 0's prev hook (after its first segment's weight DMAs, before its first chain): the
+    // reloads are older than those DMAs (the only VMEM ops issued since)
+    auto l0_wait = [&](f32x16&) MLI_LAMBDA_FI {
+      if (hd > 0) {
+        vm_wait((HEADS_PAIR ? 2 : 1) * G::template ring_ops<ROLE>());
+#pragma unroll
+        for (int q = FKS; q < 16; ++q) tie(B[q]);
+      }
+    };
     uint32_t mbits[4];
     // stg: the layer's activations go to xT (PQ: not X3, the output layer's input)
     auto relu_epi = [&](half8* out, int layer, bool stg) MLI_LAMBDA_FI {
@@ -638,7 +663,7 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
           if (t == 7) {
             u32x4* mp = reinterpret_cast<u32x4*>(a.masks) +
                         ((size_t)(hd * 4 + layer) * (S / 32) + tile) * 64 + lane;
-            __builtin_nontemporal_store(u32x4{mbits[0], mbits[1], mbits[2], mbits[3]}, mp);
+            gstore_nt(mp, u32x4{mbits[0], mbits[1], mbits[2], mbits[3]});
           }
         }
       };
@@ -658,7 +683,7 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
     constexpr int MN = TRAIN ? 1 : 0, PN = TRAIN && HEADS_DEFER ? 1 : 0;
     constexpr int X = TRAIN ? 2 : 0, X3 = PQ ? 0 : X;
     constexpr int LN = HEADS_DEFER ? X : X + MN;  // stores of a layer's last phase (epi(6) when deferred)
-    heads_layer<G, ROLE, 19, 8, X, MN, 0, HEADS_DEFER, 0, 2>(rg, lds, B, lane, bytes, NoPre{}, none, e0, pacc);
+    heads_layer<G, ROLE, 19, 8, X, MN, 0, HEADS_DEFER, 0, 2>(rg, lds, B, lane, bytes, NoPre{}, l0_wait, e0, pacc);
     heads_layer<G, ROLE, 16, 8, X, MN, PN + X, HEADS_DEFER, LN, 2>(rg, lds, A, lane, bytes, NoPre{}, fin(e0), e1, pacc);
     heads_layer<G, ROLE, 16, 8, X, MN, PN + X, HEADS_DEFER, LN, 2>(rg, lds, B, lane, bytes, NoPre{}, fin(e1), e2, pacc);
     heads_layer<G, ROLE, 16, 8, X3, MN, PN + X, HEADS_DEFER, LN, 1>(rg, lds, A, lane, bytes, NoPre{}, fin(e2), e3,
@@ -674,7 +699,7 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
         for (int i = 0; i < 3; ++i)
           if (i < no) {
             const float y = sigmoidf_acc(acc[i]);
-            a.y[8 * slot + off + i] = y;
+            gstore_f32(a.y + 8 * slot + off + i, y);
             if (PQ) gq[i] = Q4_SCALE * wgt * (y * (1.0f - y));
           }
       }
@@ -737,6 +762,14 @@ MLI_FI void rgb_bwd_body(const mli_rgb_bwd_args& a, uint8_t* lds) {
              lds + G::MASK_OFF + (L & 1) * G::MASKB + u * (G::MASKB / 2) + wave * 1024);
   };
 
+  // the sample's dz4 row (8 floats), loaded once before the ring starts: loaded per head, each
+  // conditional load waited with vmcnt(0) -- for the weight DMAs in flight as well
+  f32x4 dzv0, dzv1;
+  {
+    const f32x4* p = reinterpret_cast<const f32x4*>(a.dz4 + 8 * slot);
+    dzv0 = p[0];
+    dzv1 = p[1];
+  }
   Ring rg;
   ring_start(rg, a.wbwd, BWD_CHUNKS, bytes);
   mask_dma(0);
@@ -751,19 +784,24 @@ MLI_FI void rgb_bwd_body(const mli_rgb_bwd_args& a, uint8_t* lds) {
     const int no = hd == 2 ? 1 : 3;
     half8 z4;
     {
-      const float* dz = a.dz4 + 8 * slot + 3 * hd;
+      // dz4 columns 3 hd .. 3 hd + no - 1
+      const float d0 = hd == 0 ? dzv0[0] : hd == 1 ? dzv0[3] : dzv1[2];
+      const float d1 = hd == 0 ? dzv0[1] : dzv1[0];
+      const float d2 = hd == 0 ? dzv0[2] : dzv1[1];
 #pragma unroll
       for (int j = 0; j < 8; ++j) z4[j] = (f16)0.f;
       if (h == 0) {
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-          if (j < no) z4[j] = (f16)dz[j];
+        z4[0] = (f16)d0;
+        if (no > 1) {
+          z4[1] = (f16)d1;
+          z4[2] = (f16)d2;
+        }
       }
       // the THIN dW operand, a one-k-step fragment image (rows 0..2; NULL: the output-layer dW
       // comes from the forward's partials).  Rows j < 4 of lane half 0 are element j in both the
       // NAT and the ACC order.
       if (a.dz4T)
-        __builtin_nontemporal_store(z4, reinterpret_cast<half8*>(a.dz4T + ((size_t)hd * (S / 32) + tile) * FRAG_KS) + lane);
+        gstore_nt(reinterpret_cast<half8*>(a.dz4T + ((size_t)hd * (S / 32) + tile) * FRAG_KS) + lane, z4);
     }
     // the phase whose weight DMAs fetch the next layer's first chunk (t == 8 - DIST) issues
     // that layer's mask DMA just before them

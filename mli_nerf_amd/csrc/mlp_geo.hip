@@ -51,7 +51,7 @@ __global__ __launch_bounds__(GGeo::THREADS) void geo_bwd_kernel(mli_geo_bwd_args
       for (int j = 0; j < 3; ++j) z4[j] = (f16)dz[j];
     }
     // the output layer's dW operand: a one-k-step fragment image (rows 0..2)
-    __builtin_nontemporal_store(z4, reinterpret_cast<half8*>(a.dz4T + (size_t)tile * FRAG_KS) + lane);
+    gstore_nt(reinterpret_cast<half8*>(a.dz4T + (size_t)tile * FRAG_KS) + lane, z4);
   }
   struct MaskPre {
     decltype(mask_dma)& dma;
@@ -81,28 +81,37 @@ __global__ __launch_bounds__(GGeo::THREADS) void geo_bwd_kernel(mli_geo_bwd_args
   run_layer<G, ALL, 16, 8, 2, false>(rg, lds, B, lane, bytes, pre(2), mask_epi(A, 1, 2));
   run_layer<G, ALL, 16, 8, 2, false>(rg, lds, A, lane, bytes, NoPre{}, mask_epi(B, 0, 3));
   // feat frags (softplus output of SDF layer 1, forward scratch), one tile ahead of its use:
-  // tile 0 now, tile t+1 ahead of phase t's weight DMAs (counted as pre-issued VMEM ops)
+  // tile 0 now, tile t+1 ahead of phase t's weight DMAs (counted as pre-issued VMEM ops).  Asm
+  // loads (gload16) waited with counted vmcnts in the epilogue: compiler-visible loads among the
+  // epilogue stores made it wait vmcnt(0) -- for the phase's weight DMAs too -- every phase.
   const half8* fsrc = reinterpret_cast<const half8*>(a.feat_frag + (size_t)tile * X0_TILE) + lane;
   half8 F[2][2];
-  F[0][0] = fsrc[0];
-  F[0][1] = fsrc[64];
+  F[0][0] = gload16(fsrc);
+  F[0][1] = gload16(fsrc + 64);
   struct FeatPre {
     const half8* src;
     half8 (&F)[2][2];
     MLI_FI int count(int t) const { return t < 7 ? 2 : 0; }
     MLI_FI void issue(int t) const {
       if (t < 7) {
-        F[(t + 1) & 1][0] = src[(2 * t + 2) * 64];
-        F[(t + 1) & 1][1] = src[(2 * t + 3) * 64];
+        F[(t + 1) & 1][0] = gload16(src + (2 * t + 2) * 64);
+        F[(t + 1) & 1][1] = gload16(src + (2 * t + 3) * 64);
       }
     }
   };
+  constexpr int RO = G::template ring_ops<ALL>();
   // dX0 = W0^T dZ0: tiles 0..7 = d feat -> dZ1sdf = d feat * softplus'(z1), with
   // softplus'(z1) = 1 - exp(-100 feat) (torch: z/(z+1), z = e^{100 z1}; 1 past the threshold);
   // tile 8 = rows 256..287 (p 256..258, normal 259..261: (i=3,h=0), (i=0,h=1), (i=1,h=1))
   run_layer<G, ALL, 16, 9, 2, false>(rg, lds, B, lane, bytes, FeatPre{fsrc, F},
                                    [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
     if (t < 8) {
+      // tile t's feat loads: issued before the layer (t = 0) or at phase t - 1; after them went
+      // phase t-1's DMAs and 2 epilogue stores (t >= 1), phase t's 2 loads of tile t+1 (t < 7)
+      // and its DMAs
+      vm_wait(t == 0 ? 2 + RO : RO + 2 + (t < 7 ? 2 : 0) + RO);
+      tie(F[t & 1][0]);
+      tie(F[t & 1][1]);
       f32x16 v;
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
@@ -119,10 +128,10 @@ __global__ __launch_bounds__(GGeo::THREADS) void geo_bwd_kernel(mli_geo_bwd_args
       // undercounting only waits longer)
       float* dn = a.d_nrm + 4 * slot;
       if (h == 0) {
-        dn[0] = acc[3];
+        gstore_f32(dn, acc[3]);
       } else {
-        dn[1] = acc[0];
-        dn[2] = acc[1];
+        gstore_f32(dn + 1, acc[0]);
+        gstore_f32(dn + 2, acc[1]);
       }
     }
   });
@@ -131,8 +140,8 @@ __global__ __launch_bounds__(GGeo::THREADS) void geo_bwd_kernel(mli_geo_bwd_args
   run_layer<G, ALL, 16, 8, 2, false>(rg, lds, A, lane, bytes, NoPre{},
                                     [&](int t, const f32x16& acc) MLI_LAMBDA_FI {
     half8* dst = reinterpret_cast<half8*>(dtile) + (2 * t) * 64 + lane;
-    __builtin_nontemporal_store(acc_to_frag(acc, 0), dst);
-    __builtin_nontemporal_store(acc_to_frag(acc, 1), dst + 64);
+    gstore_nt(dst, acc_to_frag(acc, 0));
+    gstore_nt(dst + 64, acc_to_frag(acc, 1));
   });
   vm_wait(0);
 }

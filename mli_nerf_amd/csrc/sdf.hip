@@ -566,45 +566,8 @@ MLI_FI void field_points5(const float* center, const float* ray_unit, float d, i
 constexpr int BWD_WAVES = 8;  // stage-a sdf_bwd_kernel: waves per workgroup
 constexpr int LDS_SDFT_OFF = LDS_SDF;
 constexpr int LDS_DWS_OFF = LDS_SDF + MLI_SDF_T_PACK_BYTES;
-constexpr int LDS_ROWS_OFF = LDS_DWS_OFF + BWD_WAVES * 260 * 4;  // one dW/db slice per wave
-constexpr int LDS_SDF_BWD = LDS_ROWS_OFF + BWD_WAVES * 2048;        // + a 32 x 32 fp16 transpose block per wave
+constexpr int LDS_SDF_BWD = LDS_DWS_OFF + BWD_WAVES * 260 * 4;  // one dW/db slice per wave
 static_assert(LDS_SDF_BWD <= 160 * 1024, "sdf_bwd LDS");
-
-// dZ0 of one 32-sample x 32-feature n-tile (the ACC-order B fragments z0 / z1 of k-steps 2t,
-// 2t+1) -> feature-major rows dst[f * ld + s] (the wgrad operand layout; before, a frag image
-// and a separate mli_frag_rows pass: 2.7 GB of traffic per stage-a step).  Through the wave's
-// LDS block as [32 samples][32 features] (8 B chunks XOR-swizzled by sample: conflict-free b64
-// writes and transposed reads, as mlp_core.h q4_tile), then ds_read_b64_tr_b16: lane i of 16-lane
-// group g gets feature 16k + i of samples 8g .. 8g + 7 -- one 16 B store per lane and k.
-MLI_FI void dz0_rows_tile(uint8_t* xr, const half8& z0, const half8& z1, uint16_t* __restrict__ ldst, size_t kstride,
-                          int lane) {
-  // ldst: this lane's store address for k = 0 (row (lane & 15), column 8 (lane >> 4) of the
-  // tile); k = 1 is kstride (16 rows) further
-  const int c = lane & 31, h = lane >> 5;
-  // fragment element j of k-step u is feature 16u + 8(j >> 2) + 4h + (j & 3) -> 8 B chunk 4u + 2(j >> 2) + h
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const u32x4 w = __builtin_bit_cast(u32x4, u ? z1 : z0);
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      const int ch = (4 * u + 2 * jj + h) ^ ((c >> 1) & 7);
-      *reinterpret_cast<uint2*>(xr + c * 64 + ch * 8) = make_uint2(w[2 * jj], w[2 * jj + 1]);
-    }
-  }
-  asm volatile("" ::: "memory");
-  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int s0 = 8 * g + q, s1 = s0 + 4, chunk = 4 * k + p;
-    const half4 lo = ds_read_tr16(xr + s0 * 64 + (chunk ^ ((s0 >> 1) & 7)) * 8);
-    const half4 hi = ds_read_tr16(xr + s1 * 64 + (chunk ^ ((s1 >> 1) & 7)) * 8);
-    half8 v;
-    v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
-    v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-    __builtin_nontemporal_store(v, reinterpret_cast<half8*>(ldst + k * kstride));
-  }
-  asm volatile("" ::: "memory");  // the next tile's writes stay behind these reads
-}
 
 // Per sample: d sdf_i of the 5 points, then per point: layer 0 recomputed from the FIELD
 // encoding (as field_mlp_kernel), dZ0 = (w_sdf ds_i [+ W1^T dZ1 for the center]) *
@@ -701,11 +664,19 @@ __global__ __launch_bounds__(BWD_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_arg
         pz = sel_mask(mk, q[j][2], pz);
         dsp = sel_mask(mk, ds[j], dsp);
       }
-      if (h == 0) {  // layer-0 input rows p (wgrad X rows 0..2), column pi*S + m
-        const size_t col = (size_t)pi * S + m, ld = (size_t)TAPS * S;
-        a.x0_rows[col] = __builtin_bit_cast(uint16_t, (f16)px);
-        a.x0_rows[ld + col] = __builtin_bit_cast(uint16_t, (f16)py);
-        a.x0_rows[2 * ld + col] = __builtin_bit_cast(uint16_t, (f16)pz);
+      // the layer-0 weight gradient's operands (ABI 16): 32-sample tile `tile` of point pi is
+      // tile 5 tile + pi of the enc image, and of the dZ0 and p images written here
+      const size_t vt = (size_t)tile * TAPS + pi;
+      {  // p as a one-k-step NAT frag image: features 0..2 in lane half 0, the rest 0
+        half8 pv;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pv[j] = (f16)0.f;
+        if (h == 0) {
+          pv[0] = (f16)px;
+          pv[1] = (f16)py;
+          pv[2] = (f16)pz;
+        }
+        __builtin_nontemporal_store(pv, reinterpret_cast<half8*>(a.p_frag + vt * 512) + lane);
       }
       // d enc = W0_enc^T dZ0 (4 n-tiles x 16 k-steps), accumulated as dZ0's k-steps 2t, 2t+1
       // come out of tile t (no 16-fragment dZ0 array: it would need a runtime index)
@@ -714,10 +685,7 @@ __global__ __launch_bounds__(BWD_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_arg
       for (int u = 0; u < 4; ++u)
 #pragma unroll
         for (int i = 0; i < 16; ++i) de[u][i] = 0.f;
-      const size_t ld5 = (size_t)TAPS * S;
-      // column pi * S + m of [256][5S]: this lane's store address (row lane & 15, columns 8 (lane >> 4) ..)
-      uint16_t* zlane = a.dz0_rows + (size_t)pi * S + (size_t)tile * 32 + (size_t)(lane & 15) * ld5 + 8 * (lane >> 4);
-      uint8_t* xr = lds + LDS_ROWS_OFF + wave * 2048;
+      half8* ztile = reinterpret_cast<half8*>(a.dz0_frag + vt * (16 * 512)) + lane;  // 16 k-steps per tile
 #pragma unroll 1
       for (int t = 0; t < 8; ++t) {
         const uint8_t* lt = lds + opaque_v(0);
@@ -765,7 +733,10 @@ __global__ __launch_bounds__(BWD_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_arg
           }
         }
         const half8 z0 = acc_to_frag(dz, 0), z1 = acc_to_frag(dz, 1);
-        dz0_rows_tile(xr, z0, z1, zlane + (size_t)(32 * t) * ld5, 16 * ld5, lane);
+        // k-steps 2t, 2t + 1 of the tile's dZ0 image, straight from the registers (streaming: read
+        // back only by mli_wgrad)
+        __builtin_nontemporal_store(z0, ztile + (2 * t) * 64);
+        __builtin_nontemporal_store(z1, ztile + (2 * t + 1) * 64);
         const half8* fr = reinterpret_cast<const half8*>(lt + LDS_SDFT_OFF + (2 * t) * 1024) + lane;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -1198,7 +1169,7 @@ inline int sdf_bwd_blocks(int S) { return S / 256 > 1024 ? 1024 : S / 256; }
 extern "C" int mli_sdf_bwd(const mli_sdf_bwd_args* a, mli_stream_t s) {
   const int S = a->R * a->N;
   if (S <= 0) return 0;
-  if (S % 256 != 0 || !a->enc || !a->wsdf || !a->wsdf_t || !a->d_enc || !a->dz0_rows || !a->x0_rows ||
+  if (S % 256 != 0 || !a->enc || !a->wsdf || !a->wsdf_t || !a->d_enc || !a->dz0_frag || !a->p_frag ||
       !a->dw_sdf || !a->db_sdf || !a->dh0_frag || !a->d_nrm || !a->d_sdf || !a->d_grad)
     return (int)hipErrorInvalidValue;
   if (!a->partials) return (int)hipErrorInvalidValue;
@@ -1212,8 +1183,8 @@ extern "C" int mli_sdf_bwd_workspace(const mli_sdf_bwd_args* a, int64_t* bytes) 
   const int64_t S = (int64_t)a->R * a->N;
   if (S <= 0 || S % 256 != 0) return (int)hipErrorInvalidValue;
   bytes[0] = S * 640 * 4;                         // d_enc
-  bytes[1] = 5 * S * 256 * 2;                     // dz0_rows
-  bytes[2] = (int64_t)(3 + MLI_LEVELS * MLI_LEVEL_FEAT) * 5 * S * 2;  // x0_rows
+  bytes[1] = 5 * S * 256 * 2;                     // dz0_frag
+  bytes[2] = 5 * S * 16 * 2;                      // p_frag
   bytes[3] = (int64_t)sdf_bwd_blocks((int)S) * 257 * 4;             // partials
   return 0;
 }

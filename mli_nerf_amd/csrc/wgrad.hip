@@ -28,6 +28,8 @@ struct Job {
   int a_tiled, b_tiled;  // operand layout (MLI_WGRAD_LAYOUT_*): 0 rows [n][S], 1 tile-blocked
                          // [S/256][n][256], 2 / 3 frag image ACC / NAT order
   int a_kst, b_kst;      // frag images: k-steps per 32-sample tile
+  const uint16_t* b2;    // frag images: B's k-steps b2_q .. from this image (b2_kst per tile), or NULL
+  int b2_q, b2_kst;
 };
 
 // Address of (row, sample k .. k + 63) of an operand with n_rows rows: feature-major rows or the
@@ -417,10 +419,13 @@ __global__ __launch_bounds__(512) void wgrad_frag_kernel(KArgs ka) {
     const int pl = in_a ? piece : piece - TPS * KA, kq = in_a ? KA : KB;
     const int tl = pl / kq, q = pl - tl * kq;
     const int rows = in_a ? J.M : J.K, first = (in_a ? tm * BM : tn * BN) / 16;
-    const int kst = in_a ? J.a_kst : J.b_kst;
     const int qg = min(first + q, (rows + 15) / 16 - 1);
+    // (B's k-steps from b2_q on: the second image)
+    const bool sec = !in_a && J.b2 != nullptr && qg >= J.b2_q;
+    const int kst = in_a ? J.a_kst : sec ? J.b2_kst : J.b_kst;
     tstride[u] = kst * 1024;
-    sbase[u] = reinterpret_cast<const uint8_t*>(in_a ? J.a : J.b) + (size_t)tl * tstride[u] + qg * 1024;
+    sbase[u] = reinterpret_cast<const uint8_t*>(in_a ? J.a : sec ? J.b2 : J.b) + (size_t)tl * tstride[u] +
+               (sec ? qg - J.b2_q : qg) * 1024;
     odd[u] = (q & 1) << 7;
   }
   // lane (c, hh) of an even k-step's piece: 16 B at (32 hh + (c ^ 4 hh)) * 16; odd: c ^ 8 as well
@@ -709,7 +714,10 @@ inline bool job_valid(const mli_wgrad_job& j, int S) {
   if (j.a_tiled < 0 || j.a_tiled > 3 || j.b_tiled < 0 || j.b_tiled > 3) return false;
   const bool fa = is_frag(j.a_tiled), fb = is_frag(j.b_tiled);
   if (fa != fb) return false;
-  if (fa && (j.a_kst < (j.M + 15) / 16 || j.b_kst < (j.K + 15) / 16)) return false;
+  if (j.b2_rows && (!fb || j.b2_q <= 0 || j.b2_q > j.b_kst || j.b2_kst <= 0 ||
+                    j.b2_q + j.b2_kst < (j.K + 15) / 16))
+    return false;
+  if (fa && (j.a_kst < (j.M + 15) / 16 || (!j.b2_rows && j.b_kst < (j.K + 15) / 16))) return false;
   if ((j.a_tiled == MLI_WGRAD_LAYOUT_TILED || j.b_tiled == MLI_WGRAD_LAYOUT_TILED) && S % 256 != 0) return false;
   return true;
 }
@@ -732,6 +740,7 @@ int64_t plan(const mli_wgrad_args* a, int cls, bool frag, KArgs& ka) {
     J.a = j.a_rows; J.b = j.b_rows; J.M = j.M; J.K = j.K; J.ldw = j.ldw; J.dw = j.dw; J.db = j.db;
     J.a_tiled = j.a_tiled; J.b_tiled = j.b_tiled;
     J.a_kst = j.a_kst; J.b_kst = j.b_kst;
+    J.b2 = j.b2_rows; J.b2_q = j.b2_q; J.b2_kst = j.b2_kst;
     J.tiles_n = (j.K + BN - 1) / BN;
     tiles += ((j.M + BM - 1) / BM) * J.tiles_n;
   }

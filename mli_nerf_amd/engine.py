@@ -655,13 +655,18 @@ class RenderEngine:
                                     np.arange(256), gv(pre + ".weight_v"), gv(pre + ".weight_g"), gv(pre + ".bias"))
         descs.append(d)
         keep.append(kt)
-        # neural_sdf.mlp.linears.0: dZ0 x [p, enc] of the 5 points (5S samples)
+        # neural_sdf.mlp.linears.0: dZ0 x [enc, p] of the 5 points (5S samples, ABI 16): the dZ0
+        # image of mli_sdf_bwd (ACC) against the FIELD's enc image (NAT, 8 k-steps per tile) with
+        # p as a ninth k-step from the p image; packed column c < 128 is enc feature c
+        # (reference column 3 + c), 128 + i is p_i (reference column i)
         w, b = take(256, layout.SDF_K0)
-        jobs_5s.append(L.WgradJob(L.ptr(bufs["dz0_rows"]), L.ptr(bufs["x0_rows"]), 256, layout.SDF_K0, L.ptr(w),
-                                  L.ptr(b), layout.SDF_K0))
+        jobs_5s.append(L.frag_job(L.ptr(bufs["dz0_frag"]), L.ptr(bufs["enc"]), 256, layout.SDF_K0, L.ptr(w), L.ptr(b),
+                                  layout.SDF_K0, 16, 8, order=L.FRAG_ACC, b_order=L.FRAG_NAT,
+                                  b2=L.ptr(bufs["p_frag"]), b2_q=8, b2_kst=1))
         pre = "neural_sdf.mlp.linears.0"
+        kinv0 = np.concatenate([128 + np.arange(3), np.arange(128)])   # reference column -> packed column
         d, kt = self._assemble_desc(w, b, pv(pre + ".weight_v"), pv(pre + ".weight_g"), 256, layout.SDF_K0,
-                                    layout.SDF_K0, np.arange(layout.SDF_K0), gv(pre + ".weight_v"),
+                                    layout.SDF_K0, kinv0, gv(pre + ".weight_v"),
                                     gv(pre + ".weight_g"), gv(pre + ".bias"))
         descs.append(d)
         keep.append(kt)
@@ -678,6 +683,15 @@ class RenderEngine:
         self._aplan = (key, js, j5, ad, len(descs), keep, off)
         return self._aplan[1:]
 
+    def _table_grad_target(self, grad_table):
+        """The buffer mli_hash_bwd accumulates into: the int64 fixed-point workspace in
+        deterministic mode (mli_hash_bwd_workspace; 8 B per table element, 2.9 GB at 2^22, freed
+        outside that mode), else the fp32 table gradient itself."""
+        if self.deterministic:
+            return self._buf("hash_ws", (grad_table.numel(),), torch.int64)
+        self._bufs.pop("hash_ws", None)
+        return grad_table
+
     @torch.no_grad()
     def backward_a(self, st, d_rgb, flat, grad_flat, grad_table, w_eikonal, w_curvature, progress,
                    d_grad_ext=None, d_hess_ext=None):
@@ -688,7 +702,6 @@ class RenderEngine:
         rays, dists, fld, hd, comp = st
         N, R = dists.shape
         S = N * R
-        T = S // 32
         scale = float(2.0 ** round(math.log2(max(R, 1)) + 2))
         f16 = torch.float16
         dz4, d_sdf, d_grad = self._buf("dz4", (N, R, 8)), self._buf("d_sdf", (N, R)), self._buf("d_grad", (N, R, 3))
@@ -701,8 +714,8 @@ class RenderEngine:
             scale, L.ptr(dz4), L.ptr(d_sdf), L.ptr(d_grad), L.ptr(dinv), L.ptr(self.param_view(grad_flat, "s_var"))))
         b = dict(dzT=self._buf("dzT", (4, 256 * S), f16), dz4T=self._buf("dz4T", (16 * S,), f16),
                  x0T=hd["x0T"], xT=hd["xT"], dz1T=self._buf("dz1T", (256 * S,), f16),
-                 h0=fld["h0"], dz0_rows=self._buf("dz0_rows", (256, 5 * S), f16),
-                 x0_rows=self._buf("x0_rows", (layout.SDF_K0, 5 * S), f16), dws=self._buf("dws", (257,)))
+                 h0=fld["h0"], enc=fld["enc"], dz0_frag=self._buf("dz0_frag", (5 * S * 256,), f16),
+                 p_frag=self._buf("p_frag", (5 * S * 16,), f16), dws=self._buf("dws", (257,)))
         d_nrm = self._buf("d_nrm", (N, R, 4))
         dh0 = self._buf("dh0", (S * 256,), f16)
         L.call("mli_geo_bwd", L.GeoBwdArgs(R, N, L.ptr(dz4), L.ptr(self.wbwd), L.ptr(hd["masks"]), L.ptr(hd["feat"]),
@@ -714,23 +727,17 @@ class RenderEngine:
             R, N, L.ptr(rays["center"]), L.ptr(rays["ray_unit"]), L.ptr(dists), L.ptr(rays["outside"]),
             L.ptr(fld["grad"]), L.ptr(fld["hess"]), L.ptr(d_sdf), L.ptr(d_grad), L.ptr(d_nrm), L.ptr(dh0),
             L.ptr(fld["enc"]), L.ptr(self.wsdf), L.ptr(self.wsdf_t), self.eps, self.grad_den, self.hess_den,
-            float(w_eikonal), float(w_curvature), scale, L.ptr(d_enc), L.ptr(b["dz0_rows"]), L.ptr(b["x0_rows"]),
+            float(w_eikonal), float(w_curvature), scale, L.ptr(d_enc), L.ptr(b["dz0_frag"]), L.ptr(b["p_frag"]),
             L.ptr(b["dws"][:256]), L.ptr(b["dws"][256:]), L.ptr(d_grad_ext), L.ptr(d_hess_ext), L.ptr(part)))
         det = 1 if self.deterministic else 0
-        hws = None
-        if det:  # fixed-point accumulator (mli_hash_bwd_workspace), zeroed; d_table is overwritten
-            hws = self._buf("hash_ws", (grad_table.numel(),), torch.int64)
-            hws.zero_()
-        else:
-            self._bufs.pop("hash_ws", None)  # 8 B per table element (2.9 GB at 2^22): freed outside det mode
-            grad_table.zero_()
+        # (zeroed here: on a side stream beside the forward it measured 0.5-1 % slower,
+        # DESIGN.md §9.6)
+        target = self._table_grad_target(grad_table)
+        hws = target if det else None   # det: a fixed-point accumulator, zeroed; d_table is overwritten
+        target.zero_()
         L.call("mli_hash_bwd", L.HashBwdArgs(R, N, L.ptr(rays["center"]), L.ptr(rays["ray_unit"]), L.ptr(dists),
                                              L.ptr(d_enc), self.levels, self.eps, int(self.active_levels),
                                              L.ptr(grad_table), det, L.ptr(hws), grad_table.numel()))
-        # feature-major operand rows of the SDF layer-0 weight gradient (5S samples)
-        for pi in range(5):
-            L.call("mli_frag_rows", L.FragRowsArgs(L.ptr(fld["enc"]) + pi * 8 * 512 * 2, 5 * 8 * 512, T, 8, 0,
-                                                   L.ptr(b["x0_rows"]), 5 * S, pi * S, 3))
         dw_total = sum(m * k + m for m, k in [(256, layout.K0), (256, 256), (256, 256), (256, 256), (3, 256),
                                               (256, 256), (256, layout.SDF_K0)])
         b["dw"] = self._buf("dw_a", (dw_total,))

@@ -823,11 +823,6 @@ class Trainer:
         m = self.model
         m.prepare()
         m.image_width = m.image_size_train[1]
-        st = m.engine.render(data, m.s_var.detach(), m.progress, True, u=m.stratified_uniforms(data, u),
-                             W=m.image_width)
-        m._last_state = st
-        grad, lv = self._grad_buffer()
-        d_rgb = self._fused_losses(st, data, lv)[0]
         table = m.neural_sdf.tcnn_encoding.params
         if isinstance(self.optim_table, ZeroTableAdamW):
             self._grad_table_pad = self.optim_table.padded_grad(getattr(self, "_grad_table_pad", None))
@@ -835,6 +830,11 @@ class Trainer:
         elif self._grad_table is None or self._grad_table.device != table.device or \
                 self._grad_table.numel() != table.numel():
             self._grad_table = torch.empty_like(table.detach())
+        st = m.engine.render(data, m.s_var.detach(), m.progress, True, u=m.stratified_uniforms(data, u),
+                             W=m.image_width)
+        m._last_state = st
+        grad, lv = self._grad_buffer()
+        d_rgb = self._fused_losses(st, data, lv)[0]
         m.engine.backward_a(st, d_rgb, m.flat.detach(), grad, self._grad_table,
                             self.weights.get("eikonal", 0.0), self.weights.get("curvature", 0.0), m.progress)
         return st, lv

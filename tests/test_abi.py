@@ -120,7 +120,7 @@ def test_workspace_queries_match_engine_buffers():
     assert L.workspace("mli_composite_bwd_geo", L.CompositeBwdGeoArgs(R, N)) == [
         N * R * 8 * f32, N * R * f32, N * R * 3 * f32, R * f32]
     assert L.workspace("mli_sdf_bwd", L.SdfBwdArgs(R, N)) == [
-        S * 640 * f32, 5 * S * 256 * f16, layout.SDF_K0 * 5 * S * f16, 1024 * 257 * f32]
+        S * 640 * f32, 5 * S * 256 * f16, 5 * S * 16 * f16, 1024 * 257 * f32]
     loss = L.workspace("mli_stage_b_loss", L.LossArgs(R, N))
     assert loss[0] == (4 + 8 * (R // 256 + 256)) * f32 and loss[1:] == [R * 3 * f32, R * 3 * f32, R * f32, R * 3 * f32]
     assert L.workspace("mli_light_visibility", L.LightVisibilityArgs(R)) == [R * 12, R * 4, R * 4, R, R * 12]
@@ -147,11 +147,19 @@ def test_workspace_queries_match_engine_buffers():
         with pytest.raises(RuntimeError):
             L.workspace("mli_wgrad", q)
     # invalid fragment jobs: one operand a fragment image and the other not; too few k-steps per tile
+    # ABI 16 split B: b2 only with fragment images, b2_q within B's k-steps, enough k-steps in all
+    x = C.c_void_p(16)
     for bad in (L.WgradJob(None, None, 256, 256, None, None, 256, L.FRAG_ACC, L.ROWS, 16, 0),
-                L.frag_job(None, None, 256, 304, None, None, 304, 16, 16)):
+                L.frag_job(None, None, 256, 304, None, None, 304, 16, 16),
+                L.WgradJob(None, None, 256, 131, None, None, 131, L.ROWS, L.ROWS, 0, 0, x, 8, 1),
+                L.frag_job(None, None, 256, 131, None, None, 131, 16, 8, b2=x, b2_q=9, b2_kst=1),
+                L.frag_job(None, None, 256, 160, None, None, 160, 16, 8, b2=x, b2_q=8, b2_kst=1)):
         arr = (L.WgradJob * 1)(bad)
         with pytest.raises(RuntimeError):
             L.workspace("mli_wgrad", L.WgradArgs(S, 1, C.cast(arr, C.c_void_p), 7, 1, None))
+    good = (L.WgradJob * 1)(L.frag_job(None, None, 256, 131, None, None, 131, 16, 8, b_order=L.FRAG_NAT, b2=x, b2_q=8,
+                                       b2_kst=1))
+    assert L.workspace("mli_wgrad", L.WgradArgs(5 * S, 1, C.cast(good, C.c_void_p), 7, 1, None))[0] > 0
 
 
 def test_source_hash_detects_stale_library(tmp_path, monkeypatch):

@@ -214,6 +214,7 @@ def _run_a(frame, world, overlap=True, chunk=1 << 14, steps=2, monkeypatch=None,
     stub, cfg, m = _stub_setup_a()
     if install:
         stub.install(monkeypatch)
+    cfg.trainer.zero_table = False   # the replicated table path (ZeRO: test_stage_a_zero_table_matches_replicated)
     tr = Trainer(cfg, is_inference=False, model=m, world_size=world)
     tr.table_overlap, tr.table_chunk = overlap, chunk
     tr.current_iteration = 100000   # past the coarse-to-fine ramp

@@ -83,7 +83,9 @@ def test_wgrad_operand_layouts_bitwise(S):
     sums), in every launch class: BIG (256 x 256), WIDE (three jobs sharing the 304-row B operand,
     its last 32-row tile half past the image's 19 k-steps) and THIN (M = 3, a one-k-step A image)
     -- the tile-blocked images of ABI 14 (the three combinations the engine used) and the fragment
-    images of ABI 15, ACC and NAT order, with a tile stride above rows / 16.  The bias of the
+    images of ABI 15, ACC and NAT order, with a tile stride above rows / 16, and (ABI 16) an ACC
+    A against a NAT B split over two images at k-step 8 (the SDF layer-0 job: the FIELD's 8-k-step
+    enc image + the p image; K = 131 is in the set).  The bias of the
     fragment kernel is summed from the MFMA A fragments (another fp32 order): within 2e-6 of the
     rows call, and both within 1e-4 of float64."""
     _need_gpu()
@@ -91,7 +93,8 @@ def test_wgrad_operand_layouts_bitwise(S):
     from mli_nerf_amd import layout
     g = torch.Generator(device="cpu").manual_seed(11)
     shared = (torch.randn(304, S, generator=g) * 0.5).half()
-    shapes = [(256, 256, None), (256, 304, shared), (256, 304, shared), (256, 304, shared), (3, 256, None)]
+    shapes = [(256, 256, None), (256, 304, shared), (256, 304, shared), (256, 304, shared), (3, 256, None),
+              (256, 131, None)]
     ops = []
     for M, K, b in shapes:
         a = (torch.randn(M, S, generator=g) * 0.5).half()
@@ -101,6 +104,7 @@ def test_wgrad_operand_layouts_bitwise(S):
     def run(kind):
         keep, jobs, outs = [], [], []
         dev_b = {}   # one device image per distinct B (the WIDE jobs share one: SHARE_B)
+        dev_b2 = {}
         for (a, b), (M, K, _) in zip(ops, shapes):
             dw = torch.zeros(M, K, device=DEV)
             db = torch.zeros(M, device=DEV)
@@ -111,6 +115,10 @@ def test_wgrad_operand_layouts_bitwise(S):
                 A = layout.to_tiled(a) if la else a
                 B = layout.to_tiled(b) if lb else b
                 ka = kb = 0
+            elif kind == "fragsplit":
+                ka, kb, k2 = (M + 15) // 16, 8, (K - 128 + 15) // 16
+                A, B = layout.to_frag(a, ka, "acc"), layout.to_frag(b[:128], kb, "nat")
+                la, lb = L.FRAG_ACC, L.FRAG_NAT
             else:
                 order = kind[5:]
                 ka, kb = (M + 15) // 16 + 1, (K + 15) // 16 + 2   # tile strides above rows / 16
@@ -119,7 +127,13 @@ def test_wgrad_operand_layouts_bitwise(S):
             A = A.to(DEV)
             B = dev_b.setdefault(id(b), B.to(DEV))
             keep += [A, B, dw, db]
-            jobs.append(L.WgradJob(L.ptr(A), L.ptr(B), M, K, L.ptr(dw), L.ptr(db), K, la, lb, ka, kb))
+            if kind == "fragsplit":
+                B2 = dev_b2.setdefault(id(b), layout.to_frag(b[128:], k2, "nat").to(DEV))
+                keep.append(B2)
+                jobs.append(L.WgradJob(L.ptr(A), L.ptr(B), M, K, L.ptr(dw), L.ptr(db), K, la, lb, ka, kb,
+                                       L.ptr(B2), 8, k2))
+            else:
+                jobs.append(L.WgradJob(L.ptr(A), L.ptr(B), M, K, L.ptr(dw), L.ptr(db), K, la, lb, ka, kb))
             outs.append((dw, db))
         arr = (L.WgradJob * len(jobs))(*jobs)
         q = L.WgradArgs(S, len(jobs), C.cast(arr, C.c_void_p), 7, 1, None)
@@ -136,7 +150,7 @@ def test_wgrad_operand_layouts_bitwise(S):
         rw, rb = a.double() @ b.double().t(), a.double().sum(1)
         assert ((dw.double() - rw).abs().max() / rw.abs().max()).item() < 1e-4, i
         assert ((db.double() - rb).abs().max() / rb.abs().max()).item() < 1e-4, i
-    for kind in ("tiled11", "tiled01", "tiled10", "fragacc", "fragnat"):
+    for kind in ("tiled11", "tiled01", "tiled10", "fragacc", "fragnat", "fragsplit"):
         if kind.startswith("tiled") and S % 256:
             continue
         for i, ((dw, db), (bw, bb)) in enumerate(zip(run(kind), base)):
