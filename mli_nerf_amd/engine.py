@@ -14,6 +14,7 @@ neuralangelo/model.py:449-515 (sampling, NeuS alphas).
 """
 import ctypes as C
 import math
+import os
 
 import numpy as np
 import torch
@@ -140,6 +141,12 @@ class RenderEngine:
         # fixed-order reductions instead of fp32 atomics in mli_wgrad / mli_hash_bwd:
         # bit-reproducible gradients at the cost of partial-slab traffic
         self.deterministic = False
+        # mli_wgrad classes (bit mask) whose k-slices are reduced through partial slabs + an
+        # ordered sum (the deterministic mode's) instead of fp32 atomics outside that mode too:
+        # WIDE (its 80 k-slices x 3 x 256 x 304 atomic adds burst at the end of the launch).
+        # Measured (profiles/r5/slabs, same box): WIDE 0.299 -> 0.265 ms; BIG 0.831 -> 0.840 and
+        # THIN 0.143 -> 0.204 ms the other way, stage a slower with its 5S job on slabs.
+        self.wgrad_slab_classes = int(os.environ.get("MLI_WGRAD_SLABS", "2"))
         # stage-b training: the output layers' dW from per-tile partials the heads forward forms
         # while X3 is in registers (mli_rgb_fwd PQ mode + mli_dw4) instead of X3 through HBM and
         # the THIN split-K GEMM; needs N % 32 == 0 (a 32-sample tile within one ray)
@@ -559,14 +566,17 @@ class RenderEngine:
         """mli_wgrad over `classes` (separate launches, timed separately); deterministic mode:
         partial slabs in a workspace sized by mli_wgrad_workspace, else fp32 atomics into the
         zeroed outputs (the caller zeroes them)."""
-        det = 1 if self.deterministic else 0
+        slab = 7 if self.deterministic else self.wgrad_slab_classes
+        need = sum(classes) & slab
         ws = None
-        if det:
-            q = L.WgradArgs(S, len(jobs), C.cast(jobs, C.c_void_p), sum(classes), 1, None)
+        if need:
+            q = L.WgradArgs(S, len(jobs), C.cast(jobs, C.c_void_p), need, 1, None)
             nbytes = L.workspace("mli_wgrad", q)[0]
             ws = self._buf("wgrad_ws", (max(nbytes, 4) // 4,))
-        for cls in classes:
-            L.call("mli_wgrad", L.WgradArgs(S, len(jobs), C.cast(jobs, C.c_void_p), cls, det, L.ptr(ws)))
+        for cls in classes:   # (a mask of several classes: its slab and atomic classes apart)
+            for part, det in ((cls & ~slab, 0), (cls & slab, 1)):
+                if part:
+                    L.call("mli_wgrad", L.WgradArgs(S, len(jobs), C.cast(jobs, C.c_void_p), part, det, L.ptr(ws)))
 
     @torch.no_grad()
     def backward(self, st, d_rgb, d_o_r, d_o_s, d_o_re, flat, sdf_l1, grad_out, dz4=None):
