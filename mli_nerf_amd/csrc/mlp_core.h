@@ -36,8 +36,9 @@ constexpr int X0_TILE = X0_KS * FRAG_KS;
 constexpr int Q4_SLOT = 257 * 16;  // one wave's output-layer partials Q in LDS (PQ mode, q4_tile)
 constexpr int DIST = 2;                 // chunks in flight ahead of the one being read (3: no gain)
 // Paired phases (run_layer_p): a barrier every second n-tile, the weight ring 4 slots deep.
-// Measured (profiles/r5/pair, alternating on one box): rgb_fwd (train) 1.025 -> 0.929 ms, rgb_bwd
-// 0.737 -> 0.657 ms, step 3.93 -> 3.80 ms against a barrier per n-tile (MLI_HEADS_PAIR=0).
+// Measured (profiles/r5/pairq, alternating on one box, against a barrier per n-tile --
+// MLI_HEADS_PAIR=0): rgb_fwd (train) 1.005-1.009 vs 1.030-1.042 ms, rgb_bwd 0.677-0.710 vs
+// 0.716-0.745 ms, the step within noise.
 #ifndef MLI_HEADS_PAIR
 #define MLI_HEADS_PAIR 1
 #endif
