@@ -717,7 +717,10 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
 // 0.86 vs 0.81 ms -- the weight chunks stream through LDS once per workgroup, so halving the
 // workgroup doubles the ring DMA and LDS-write work per sample.
 // weight-fragment read depth of the training kernels (PF 3 / 4 / 6 measured: profiles/r3/heads_pf)
-constexpr int HEADS_PF = 4;
+#ifndef MLI_HEADS_PF
+#define MLI_HEADS_PF 4
+#endif
+constexpr int HEADS_PF = MLI_HEADS_PF;
 typedef Geo<8, 20, true> GFwd;             // eval forward
 typedef Geo<8, 20, true, HEADS_PF> GFwdT;  // training forward (same layout)
 typedef Geo<8, 17, true, HEADS_PF> GBwd;

@@ -1,0 +1,48 @@
+"""tools/asm_audit.py and tools/kinfo.py on small hand-written assembly (CPU): the audit flags a
+compiler instruction that names an asm load's destination before its counted wait, and an asm
+16-byte store without s_nop; kinfo counts the compiler's vmcnt waits and skips asm ones
+(the vmcnt(0) drains)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tools"))
+import asm_audit  # noqa: E402
+import kinfo  # noqa: E402
+
+HEAD = "_ZN3fooEv:\n"
+TAIL = "\t.size\t_ZN3fooEv, 4\n"
+
+
+def _write(tmp_path, body):
+    p = tmp_path / "k.s"
+    p.write_text(HEAD + body + TAIL)
+    return str(p)
+
+
+def test_audit_flags_early_use_of_asm_load(tmp_path):
+    body = ("\t;;#ASMSTART\n\tds_read_b64_tr_b16 v[4:5], v1 offset:0\n\t;;#ASMEND\n"
+            "\tv_mov_b32_e32 v9, v5\n"
+            "\t;;#ASMSTART\n\ts_waitcnt lgkmcnt(0)\n\t;;#ASMEND\n")
+    assert asm_audit.audit(_write(tmp_path, body)) == 1
+
+
+def test_audit_accepts_use_after_wait(tmp_path):
+    body = ("\t;;#ASMSTART\n\tglobal_load_dwordx4 v[4:7], v[0:1], off\n\t;;#ASMEND\n"
+            "\tv_add_u32_e32 v9, v10, v11\n"
+            "\t;;#ASMSTART\n\ts_waitcnt vmcnt(2)\n\t;;#ASMEND\n"
+            "\tv_mov_b32_e32 v9, v5\n"
+            "\t;;#ASMSTART\n\tglobal_store_dwordx4 v[0:1], v[4:7], off nt\n\ts_nop 1\n\t;;#ASMEND\n")
+    assert asm_audit.audit(_write(tmp_path, body)) == 0
+
+
+def test_audit_flags_store_without_nop(tmp_path):
+    body = "\t;;#ASMSTART\n\tglobal_store_dwordx4 v[0:1], v[4:7], off nt\n\t;;#ASMEND\n"
+    assert asm_audit.audit(_write(tmp_path, body)) == 1
+
+
+def test_kinfo_counts_compiler_waits_only(tmp_path, capsys):
+    body = ("\ts_waitcnt vmcnt(0)\n\tv_mfma_f32_32x32x16_f16 a[0:15], v[0:3], v[4:7], a[0:15]\n"
+            "\t;;#ASMSTART\n\ts_waitcnt vmcnt(0)\n\t;;#ASMEND\n\ts_barrier\n\tscratch_load_dword v1, off, off\n")
+    kinfo.main(_write(tmp_path, body), "foo")
+    out = capsys.readouterr().out
+    assert "scratch 1 mfma 1 barrier 1" in out and "'s_waitcnt vmcnt(0)': 1" in out
