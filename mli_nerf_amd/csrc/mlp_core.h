@@ -201,8 +201,8 @@ MLI_FI float mask_bit(float x, uint32_t bits, int bit) {
 // two weight fragments ahead and waits lgkmcnt(0) before every MFMA pair, so each pair pays the
 // LDS latency); PF > 0: the fragments are read PF ahead, one read issued after each MFMA (the
 // order pinned by sched_group_barrier).  Measured (profiles/r3/pf): PF = 4 takes the training
-// heads forward 1.19 -> 1.15 ms and rgb_bwd 0.885 -> 0.86 ms; the eval forward is slower with
-// it (3.85 -> 3.95 ms per 20000-ray chunk), so it keeps PF = 0.
+// heads forward 1.19 -> 1.15 ms and rgb_bwd 0.885 -> 0.86 ms; the eval forward was slower with
+// it then (3.85 -> 3.95 ms per 20000-ray chunk) and took PF = 4 in round 5 (GFwd below).
 template <int KS, int PF = 0>
 MLI_FI f32x16 chunk_mma(const uint8_t* chunk, const half8* X, int lane) {
   const int h = lane >> 5;
@@ -721,7 +721,9 @@ MLI_FI void rgb_fwd_body(const mli_rgb_fwd_args& a, uint8_t* lds) {
 #define MLI_HEADS_PF 4
 #endif
 constexpr int HEADS_PF = MLI_HEADS_PF;
-typedef Geo<8, 20, true> GFwd;             // eval forward
+// (the eval forward took PF = 0 until round 5: with the paired phases PF = 4 is faster there too,
+// 800 x 800 inference 2.540-2.548 -> 2.572-2.575 M rays/s, profiles/r5/evalpf)
+typedef Geo<8, 20, true, HEADS_PF> GFwd;   // eval forward
 typedef Geo<8, 20, true, HEADS_PF> GFwdT;  // training forward (same layout)
 typedef Geo<8, 17, true, HEADS_PF> GBwd;
 
