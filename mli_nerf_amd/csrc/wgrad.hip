@@ -583,8 +583,19 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(RArgs r) {
   const int64_t MK = (int64_t)r.M[j] * r.K[j], stride = MK + r.M[j];
   if (loc >= MK && r.db[j] == nullptr) return;
   const float* p = r.part + r.base[j] + loc;
+  // 16 slices' loads in flight, summed in slice order (the same fixed order: bit-identical).
+  // The plain loop was one load -> vmcnt(0) -> add per slice: 80 round trips, 150 us for the
+  // WIDE slabs beside the prefetched geometry (profiles/r5/final2 trace).
   float acc = 0.f;
-  for (int sp = 0; sp < r.n_split; ++sp) acc += p[sp * stride];
+  int sp = 0;
+  for (; sp + 16 <= r.n_split; sp += 16) {
+    float v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = p[(int64_t)(sp + q) * stride];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc += v[q];
+  }
+  for (; sp < r.n_split; ++sp) acc += p[(int64_t)sp * stride];
   if (loc < MK) {
     const int row = (int)(loc / r.K[j]), col = (int)(loc - (int64_t)row * r.K[j]);
     r.dw[j][(size_t)row * r.ldw[j] + col] = acc;
