@@ -705,12 +705,16 @@ constexpr int WIDE_DMA = 2, WIDE_BKD = 64;
 // BIG through the same ring, 2 stages of 64 samples: 0.898 -> 0.847 ms (register staging of 64
 // samples before; the ring at 32-sample stages -- 64 B row segments -- measured 0.998 ms)
 constexpr int BIG_DMA = 2;
-// the fragment-image kernel (every class): FRAG_NBUF stages of FRAG_TPS 32-sample tiles
+// the fragment-image kernel (every class): FRAG_NBUF stages of FRAG_TPS 32-sample tiles.
+// 4 stages of one tile (three in flight): measured slower than 2 x 2 tiles while every stage
+// waited for the next one's DMAs (BIG 0.86 -> 0.99 ms, profiles/r5/tps); with the waits counted,
+// a little faster (BIG 0.823 -> 0.814-0.817, WIDE 0.249-0.261 -> 0.245-0.247 ms,
+// profiles/r5/tps2)
 #ifndef MLI_FRAG_TPS
-#define MLI_FRAG_TPS 2
+#define MLI_FRAG_TPS 1
 #endif
 #ifndef MLI_FRAG_NBUF
-#define MLI_FRAG_NBUF 2
+#define MLI_FRAG_NBUF 4
 #endif
 constexpr int FRAG_TPS = MLI_FRAG_TPS, FRAG_NBUF = MLI_FRAG_NBUF;
 
