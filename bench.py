@@ -299,7 +299,7 @@ def cpu_baseline(cfg, R_cpu, steps, threads, stage_a=None):
             times.append(time.perf_counter() - t0)
         progress("cpu baseline step %d/%d: %.2f s" % (i + 1, steps + 2, time.perf_counter() - t0))
     t = sum(times) / len(times)
-    return dict(value=R_cpu / t, unit="rays/s", cores=threads, kind="port",
+    return dict(value=R_cpu / t, unit="rays/s", cores=threads, kind="port", per_thread=R_cpu / t / threads,
                 sample="oracle fwd+bwd stage-%s, %d rays x %d samples, full hash table, %d timed steps "
                        "after 2 warm-up, torch fp32 on %d host threads" % ("a" if stage_a else "b", R_cpu,
                                                                           pcfg.n_samples, steps, threads),
@@ -345,12 +345,23 @@ def host_cpu():
 
 
 def cpu_threads(args):
+    """(threads, host info); host["threads_rule"] says which count was taken and why (VERDICT r5
+    item 8): SURVEY §8(d) asks for the physical cores, and the affinity mask's physical cores are
+    that count; on the GPU box a one-GPU job is allotted a share of the host (OMP_NUM_THREADS, 16)
+    and the rest of the cores run other jobs, so the baseline takes the smaller of the two and the
+    record says so (the per-thread rate is reported beside it)."""
     hc = host_cpu()
     if args.cpu_threads:
+        hc["threads_rule"] = "--cpu-threads %d (explicit)" % args.cpu_threads
         return args.cpu_threads, hc
     n = hc["affinity_physical_cores"] or 1
-    if hc["job_cpu_share"]:
-        n = min(n, hc["job_cpu_share"])
+    rule = "affinity physical cores (%d)" % n
+    if hc["job_cpu_share"] and hc["job_cpu_share"] < n:
+        rule = ("job CPU share OMP_NUM_THREADS=%d < affinity physical cores %d (SURVEY 8d's count): the box "
+                "allots %d CPUs to this one-GPU job, the other cores belong to other jobs" % (
+                    hc["job_cpu_share"], n, hc["job_cpu_share"]))
+        n = hc["job_cpu_share"]
+    hc["threads_rule"] = rule
     return n, hc
 
 

@@ -52,7 +52,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mli_stream_t; /* == hipStream_t */
 
-#define MLI_ABI_VERSION 16
+#define MLI_ABI_VERSION 17
 #define MLI_HIDDEN 256
 #define MLI_LEVELS 16
 #define MLI_LEVEL_FEAT 8
@@ -614,19 +614,24 @@ typedef struct {
   int n_layers;
   const mli_assemble_layer* layers; /* DEVICE array */
   float inv_scale;
+  int zero_dw;            /* ABI 17: 1 = every dw / db element read is left 0 (the next split-K
+                             accumulation adds into a zeroed buffer without a fill launch) */
 } mli_assemble_args;
 int mli_grad_assemble(const mli_assemble_args* a, mli_stream_t s);
 
 /* AdamW over one flat fp32 parameter buffer (torch.optim.AdamW semantics,
  * imaginaire/trainers/utils/get_trainer.py:106-150, base.yaml:117-127). */
 typedef struct {
-  float* p; const float* g; float* m; float* v;
+  float* p; float* g; float* m; float* v;
   int64_t n;
   double lr, beta1, beta2, eps, weight_decay; /* double, as torch's Python scalars: the step
                            coefficients (1 - beta, lr / bias correction ...) are formed in double
                            and rounded to fp32 once, as torch.optim.AdamW does */
   int step;               /* 1-based step after increment */
   uint16_t* p16;          /* optional fp16 copy of the updated p (hash-table shadow), or NULL */
+  int zero_grad;          /* ABI 17: 1 = leave g all zero for the next scatter (g[i] = 0 stored
+                           only where g[i] != 0: the sparse hash-table gradient's touched lines,
+                           instead of a dense fill of the whole buffer before mli_hash_bwd) */
 } mli_adamw_args;
 int mli_adamw(const mli_adamw_args* a, mli_stream_t s);
 

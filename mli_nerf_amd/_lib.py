@@ -138,12 +138,13 @@ class AssembleLayer(C.Structure):
 
 
 class AssembleArgs(C.Structure):
-    _fields_ = [("n_layers", I32), ("layers", P), ("inv_scale", F32)]
+    _fields_ = [("n_layers", I32), ("layers", P), ("inv_scale", F32), ("zero_dw", I32)]
 
 
 class AdamwArgs(C.Structure):
     _fields_ = [("p", P), ("g", P), ("m", P), ("v", P), ("n", I64), ("lr", F64), ("beta1", F64),
-                ("beta2", F64), ("eps", F64), ("weight_decay", F64), ("step", I32), ("p16", P)]
+                ("beta2", F64), ("eps", F64), ("weight_decay", F64), ("step", I32), ("p16", P),
+                ("zero_grad", I32)]
 
 
 class CastArgs(C.Structure):
@@ -200,7 +201,7 @@ class FragRowsArgs(C.Structure):
                 ("ld", I64), ("col0", I64), ("row0", I32)]
 
 
-ABI_VERSION = 16  # include/mli_hip.h MLI_ABI_VERSION
+ABI_VERSION = 17  # include/mli_hip.h MLI_ABI_VERSION
 
 ENTRY_POINTS = {
     "mli_rays": RaysArgs, "mli_hashgrid_fwd": HashgridArgs, "mli_sdf": SdfArgs,

@@ -68,16 +68,27 @@ __global__ __launch_bounds__(256) void pack_kernel(const mli_pack_layer* layers,
 // dW_ref[n][c] = dW_pack[n][kinv[c]] * inv_scale; weight-norm backward:
 //   dg[n] = sum_c dW_ref[n][c] * v[n][c] / ||v_n||
 //   dv[n][c] = g[n] / ||v_n|| * (dW_ref[n][c] - dg[n] * v[n][c] / ||v_n||)
-__global__ __launch_bounds__(256) void assemble_kernel(const mli_assemble_layer* layers, float inv_scale) {
+// zero_dw (ABI 17): each dW / db element is set to 0 right after its last read, so the next
+// split-K accumulation finds the buffer zeroed (no fill launch; the packed padding columns are
+// never read and stay 0: their operand rows are exact zeros).
+__global__ __launch_bounds__(256) void assemble_kernel(const mli_assemble_layer* layers, float inv_scale,
+                                                       int zero_dw) {
   const mli_assemble_layer& L = layers[blockIdx.y];
   const int n = blockIdx.x;
   if (n >= L.n_out) return;
   __shared__ float red[2][256];
   const int tid = threadIdx.x;
+  float* dwz = const_cast<float*>(L.dw);
   if (L.plain) {  // plain nn.Linear (linear_sdf, mlp.py:50): no weight-norm backward
-    for (int c = tid; c < L.k_ref; c += 256)
-      L.grad_v[(size_t)n * L.k_ref + c] = L.dw[(size_t)n * L.k_pack + L.kinv[c]] * inv_scale;
-    if (tid == 0) L.grad_b[n] = L.db[n] * inv_scale;
+    for (int c = tid; c < L.k_ref; c += 256) {
+      const size_t i = (size_t)n * L.k_pack + L.kinv[c];
+      L.grad_v[(size_t)n * L.k_ref + c] = L.dw[i] * inv_scale;
+      if (zero_dw) dwz[i] = 0.f;
+    }
+    if (tid == 0) {
+      L.grad_b[n] = L.db[n] * inv_scale;
+      if (zero_dw) const_cast<float*>(L.db)[n] = 0.f;
+    }
     return;
   }
   const float* vr = L.v + (size_t)n * L.k_ref;
@@ -101,12 +112,15 @@ __global__ __launch_bounds__(256) void assemble_kernel(const mli_assemble_layer*
   const float dg = red[1][0] / nrm;
   const float gs = L.g[n] / nrm;
   for (int c = tid; c < L.k_ref; c += 256) {
-    const float d = L.dw[(size_t)n * L.k_pack + L.kinv[c]] * inv_scale;
+    const size_t i = (size_t)n * L.k_pack + L.kinv[c];
+    const float d = L.dw[i] * inv_scale;
     L.grad_v[(size_t)n * L.k_ref + c] = gs * (d - dg * vr[c] / nrm);
+    if (zero_dw) dwz[i] = 0.f;   // (this thread's last read of element i)
   }
   if (tid == 0) {
     L.grad_g[n] = dg;
     L.grad_b[n] = L.db[n] * inv_scale;
+    if (zero_dw) const_cast<float*>(L.db)[n] = 0.f;
   }
 }
 
@@ -133,11 +147,15 @@ __global__ __launch_bounds__(256) void adamw_kernel(mli_adamw_args a, AdamwCoef 
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n) return;
   float p = a.p[i], m = a.m[i], v = a.v[i];
-  adamw_one(c, p, a.g[i], m, v);
+  const float g = a.g[i];
+  adamw_one(c, p, g, m, v);
   a.p[i] = p;
   a.m[i] = m;
   a.v[i] = v;
   if (a.p16) a.p16[i] = __builtin_bit_cast(uint16_t, (f16)p);  // fp16 gather shadow (hash table)
+  // the consumed gradient left zero for the next accumulation: only the entries the sparse
+  // scatter touched are written (a masked store), not the whole buffer
+  if (a.zero_grad && g != 0.0f) a.g[i] = 0.0f;
 }
 
 __global__ __launch_bounds__(256) void cast_kernel(mli_cast_args a) {
@@ -167,7 +185,7 @@ extern "C" int mli_pack_workspace(const mli_pack_args* a, int64_t* bytes) {
 
 extern "C" int mli_grad_assemble(const mli_assemble_args* a, mli_stream_t s) {
   hipLaunchKernelGGL(assemble_kernel, dim3(256, a->n_layers), dim3(256), 0, (hipStream_t)s,
-                     a->layers, a->inv_scale);
+                     a->layers, a->inv_scale, a->zero_dw);
   MLI_LAUNCH_CHECK();
 }
 

@@ -99,6 +99,12 @@ class _GeometryLane(dict):
         return dict.pop(d, k, *default) if d is self else d.pop(k, *default)
 
 
+# stage-b weight-gradient classes in launch order and the head layers each one completes
+# (mli_dw4 / THIN: the output layers; BIG: the hidden 256 x 256 layers; WIDE: layer 0)
+GRAD_CLASSES = ("out", "big", "wide")
+GRAD_CLASS_LAYERS = {"out": (4,), "big": (1, 2, 3), "wide": (0,)}
+
+
 def _to_device_structs(structs, device):
     raw = b"".join(bytes(s) for s in structs)
     return torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
@@ -119,6 +125,11 @@ class RenderEngine:
         self.set_normal_eps(normal_eps(cfg.levels, cfg.min_logres, cfg.max_logres))
         self.active_levels = cfg.levels
         self.table16 = None
+        # data_ptr of a table-gradient buffer the last table AdamW left all zero (mli_adamw zero_grad),
+        # of the split-K dW buffer the last assemble left zero (zero_dw), of the zeroed head outputs
+        self.table_grad_clean = None
+        self._dw_zero = None
+        self._y_zeroed = None
         self.wsdf = torch.empty(65536 + 5 * 1024 + 16, dtype=torch.uint8, device=self.device)
         self.fplan, fbytes = layout.fwd_plan(self.head_specs)
         self.bplan, bbytes = layout.geo_plan() if stage == "a" else layout.bwd_plan()
@@ -354,19 +365,22 @@ class RenderEngine:
                              "reference configs' batches are: 4096 / 8192 rays x 128 / 192 samples)" % (R, N))
         nh = len(self.head_specs)
         y = self._buf("y", (N, R, 8))
-        if nh == 1:
-            y.zero_()  # o_r / o_s slots the single head does not write (composite reads them)
+        if nh == 1 and self._y_zeroed != y.data_ptr():
+            # o_r / o_s slots the single head never writes (composite reads them): zeroed once per
+            # allocation (rows of 8 at any shape, so they stay zero)
+            y.zero_()
+            self._y_zeroed = y.data_ptr()
         # the x0 image: SDF feature (k-steps 0..15 of each 32-sample tile) + in training the extras
         # (16..18); the WIDE dW operand (ABI 15)
         feat = self._buf("feat", (S * layout.K0,), torch.float16)
         xT = masks = w = q4 = None
         pq = s_var is not None and self.pq_mode(N, training)
         if training and self.stage == "b" and not self.deterministic:
-            # the split-K dW accumulators of this lane's backward, zeroed here at the start of the
-            # step, where the GPU is not shared with the prefetched geometry (before the heads
-            # backward the fill competed with the sampling rounds: 5 -> 19 us)
-            self._buf("dw", (self._dw_total(),)).zero_()
-            self._bufs["dw_clean"] = True
+            # the split-K dW accumulators of this lane's backward: left zero by the last
+            # mli_grad_assemble (zero_dw, ABI 17), else zeroed here at the start of the step, where
+            # the GPU is not shared with the prefetched geometry (before the heads backward the
+            # fill competed with the sampling rounds: 5 -> 19 us)
+            self._zero_once(self._buf("dw", (self._dw_total(),)))
         if training:
             xT = self._buf("xT", (nh, 3 if pq else 4, S * 256), torch.float16)  # ACC frag images
             masks = self._buf("masks", (nh, 4, S // 32, 64, 4), torch.int32)
@@ -557,7 +571,11 @@ class RenderEngine:
                                                 L.ptr(self.param_view(grad_out, pre + ".weight_g")),
                                                 L.ptr(self.param_view(grad_out, pre + ".bias")), None))
         job_arr = (L.WgradJob * len(jobs))(*jobs)
-        ad = _to_device_structs(assemble, self.device)
+        # descriptors in dW-class order (one block row per layer, independent): the output layers
+        # (mli_dw4 / THIN), the hidden layers (BIG), the layer-0 ones (WIDE), so that a class's
+        # layers can be assembled -- and their gradient all-reduced -- as soon as its dW is done
+        order = [h * 5 + li for cls in GRAD_CLASSES for li in GRAD_CLASS_LAYERS[cls] for h in range(len(layout.HEADS))]
+        ad = _to_device_structs([assemble[i] for i in order], self.device)
         plan = (job_arr, ad, (dw4, db4, k4))
         self._wplans[key] = plan
         return plan
@@ -579,10 +597,12 @@ class RenderEngine:
                     L.call("mli_wgrad", L.WgradArgs(S, len(jobs), C.cast(jobs, C.c_void_p), part, det, L.ptr(ws)))
 
     @torch.no_grad()
-    def backward(self, st, d_rgb, d_o_r, d_o_s, d_o_re, flat, sdf_l1, grad_out, dz4=None):
+    def backward(self, st, d_rgb, d_o_r, d_o_s, d_o_re, flat, sdf_l1, grad_out, dz4=None, on_class=None):
         """Gradient of the loss w.r.t. the trainable head parameters into grad_out (flat), from
         d loss / d (rgb, o_r, o_s, o_re) -- or from ``dz4`` when composite_loss already ran the
-        composite backward (the d_* are then unused; in PQ mode it also wrote the per-ray D)."""
+        composite backward (the d_* are then unused; in PQ mode it also wrote the per-ray D).
+        ``on_class(name)``: called (host side, in stream order) once the gradient of the layers
+        of dW class ``name`` (GRAD_CLASSES) is complete in grad_out."""
         rays, dists, fld, hd, comp = st
         N, R = dists.shape
         S = N * R
@@ -598,8 +618,10 @@ class RenderEngine:
                                                            L.ptr(self._buf("dray", (R, 8)) if pq else None)))
         dz4T = None if pq else self._buf("dz4T", (3, S * 16), torch.float16)  # one-k-step frag images
         dwbuf = self._buf("dw", (self._dw_total(),))
-        if not self.deterministic and not self._bufs.pop("dw_clean", False):
-            dwbuf.zero_()  # split-K partials add into it (fp32 atomics); heads() zeroes it once per render
+        zero_dw = 0 if self.deterministic else 1
+        if zero_dw:
+            self._zero_once(dwbuf)   # split-K partials add into it (fp32 atomics)
+            self._dw_zero = None     # (accumulating from here on, until the assemble zeroes it)
         dzT = self._buf("dzT", (3, 4, S * 256), torch.float16)  # ACC frag images
         L.call("mli_rgb_bwd", L.RgbBwdArgs(R, N, L.ptr(dz4), L.ptr(self.wbwd), L.ptr(hd["masks"]), L.ptr(dzT),
                                            L.ptr(dz4T)))
@@ -607,16 +629,47 @@ class RenderEngine:
         if self.gate_wgrad:  # Trainer.prefetch(gate="wgrad"): next geometry may start here
             self.gate_event = torch.cuda.Event()
             self.gate_event.record()
-        if pq:
-            args = L.Dw4Args(R, N, 3, L.ptr(hd["q4"]), L.ptr(self._bufs["dray"]), scale / L.Q4_SCALE,
-                             (C.c_void_p * 3)(*dw4), (C.c_void_p * 3)(*db4), (C.c_int * 3)(*k4), None)
-            args.workspace = L.ptr(self._buf("dw4_ws", (L.workspace("mli_dw4", args)[0] // 4,)))
-            L.call("mli_dw4", args)
-            self._wgrad(S, jobs, (1, 2))  # BIG, WIDE
-        else:
-            self._wgrad(S, jobs, (1, 2, 4))  # BIG, WIDE, THIN launch classes
-        L.call("mli_grad_assemble", L.AssembleArgs(15, L.ptr(ad), 1.0 / scale))
+        if on_class is None:   # one assemble launch once every dW class is done
+            if pq:
+                self._dw4(R, N, hd, scale, dw4, db4, k4)
+                self._wgrad(S, jobs, (1, 2))  # BIG, WIDE
+            else:
+                self._wgrad(S, jobs, (1, 2, 4))  # BIG, WIDE, THIN launch classes
+            L.call("mli_grad_assemble", L.AssembleArgs(15, L.ptr(ad), 1.0 / scale, zero_dw))
+            self._dw_zero = dwbuf.data_ptr() if zero_dw else None
+            return grad_out
+        # per class (the DDP bucket order of the overlapped all-reduce): dW, its layers'
+        # assemble, then on_class(name) -- the caller issues that class's reduction while the
+        # next class's dW runs
+        nh, sz = len(layout.HEADS), C.sizeof(L.AssembleLayer)
+        first = 0
+        for cls in GRAD_CLASSES:
+            if cls == "out":
+                if pq:
+                    self._dw4(R, N, hd, scale, dw4, db4, k4)
+                else:
+                    self._wgrad(S, jobs, (4,))
+            else:
+                self._wgrad(S, jobs, (1,) if cls == "big" else (2,))
+            n = nh * len(GRAD_CLASS_LAYERS[cls])
+            L.call("mli_grad_assemble", L.AssembleArgs(n, L.ptr(ad) + first * sz, 1.0 / scale, zero_dw))
+            first += n
+            on_class(cls)
+        self._dw_zero = dwbuf.data_ptr() if zero_dw else None
         return grad_out
+
+    def _zero_once(self, buf):
+        """Zero a split-K dW accumulator unless the last mli_grad_assemble left it zero."""
+        if self._dw_zero != buf.data_ptr():
+            buf.zero_()
+            self._dw_zero = buf.data_ptr()
+
+    def _dw4(self, R, N, hd, scale, dw4, db4, k4):
+        """PQ mode: the output layers' dW / db from the forward's q4 and the per-ray D."""
+        args = L.Dw4Args(R, N, 3, L.ptr(hd["q4"]), L.ptr(self._bufs["dray"]), scale / L.Q4_SCALE,
+                         (C.c_void_p * 3)(*dw4), (C.c_void_p * 3)(*db4), (C.c_int * 3)(*k4), None)
+        args.workspace = L.ptr(self._buf("dw4_ws", (L.workspace("mli_dw4", args)[0] // 4,)))
+        L.call("mli_dw4", args)
 
 
     # ------------------------------------------------------------------ stage a backward
@@ -744,7 +797,12 @@ class RenderEngine:
         # DESIGN.md §9.6)
         target = self._table_grad_target(grad_table)
         hws = target if det else None   # det: a fixed-point accumulator, zeroed; d_table is overwritten
-        target.zero_()
+        # the fp32 gradient is accumulated into: zeroed here, unless the last table AdamW consumed
+        # this very buffer and left it zero (mli_adamw zero_grad, ABI 17: only the touched entries
+        # are rewritten, not a 1.46 GB fill per step)
+        if det or self.table_grad_clean != grad_table.data_ptr():
+            target.zero_()
+        self.table_grad_clean = None
         L.call("mli_hash_bwd", L.HashBwdArgs(R, N, L.ptr(rays["center"]), L.ptr(rays["ray_unit"]), L.ptr(dists),
                                              L.ptr(d_enc), self.levels, self.eps, int(self.active_levels),
                                              L.ptr(grad_table), det, L.ptr(hws), grad_table.numel()))
@@ -752,9 +810,12 @@ class RenderEngine:
                                               (256, 256), (256, layout.SDF_K0)])
         b["dw"] = self._buf("dw_a", (dw_total,))
         js, j5, ad, n_desc, _, _ = self._plan_a(b, flat, grad_flat, S)
-        if not self.deterministic:
-            b["dw"].zero_()
+        zero_dw = 0 if self.deterministic else 1
+        if zero_dw:   # left zero by the last assemble (ABI 17), else one fill
+            self._zero_once(b["dw"])
+            self._dw_zero = None
         self._wgrad(S, js, (7,))
         self._wgrad(5 * S, j5, (7,))
-        L.call("mli_grad_assemble", L.AssembleArgs(n_desc, L.ptr(ad), 1.0 / scale))
+        L.call("mli_grad_assemble", L.AssembleArgs(n_desc, L.ptr(ad), 1.0 / scale, zero_dw))
+        self._dw_zero = b["dw"].data_ptr() if zero_dw else None
         return grad_flat, grad_table

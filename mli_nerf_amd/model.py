@@ -322,7 +322,10 @@ class Model(torch.nn.Module):
         src = state_dict.get(self.TABLE_KEY)
         if src is not None and src.numel() != self.neural_sdf.tcnn_encoding.params.numel():
             self._adopt_table_size(src.numel())
-        return super().load_state_dict(state_dict, strict=strict, assign=assign)
+        res = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        if src is not None:
+            self.table_sharded_stale = False   # the whole fp32 table was just written
+        return res
 
     def _adopt_table_size(self, numel):
         from .hashgrid import SCALE_RULES
@@ -385,6 +388,12 @@ class Model(torch.nn.Module):
             table = sdf.tcnn_encoding.params
             ver = (table._version, table.data_ptr())
             if ver != self._sdf_version:
+                if getattr(self, "table_sharded_stale", False):
+                    # ZeRO (trainer.ZeroTableAdamW): outside this rank's shard the fp32 master is
+                    # older than the fp16 shadow the kernels read; re-casting it would revert the
+                    # other ranks' updates
+                    raise RuntimeError("the hash table is ZeRO-sharded and not gathered: call "
+                                       "trainer.sync_table() on every rank before rebuilding the engine")
                 eng.load_table(table.detach())
                 self._sdf_version = ver
             eng.pack_sdf(*pack_args)

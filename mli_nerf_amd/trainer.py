@@ -117,14 +117,16 @@ class FusedAdamW:
         self.v = torch.zeros_like(flat.detach())
         self.step_count = 0
 
-    def step(self, grad, lr, p16=None, ranges=None, before=None):
+    def step(self, grad, lr, p16=None, ranges=None, before=None, zero_grad=False):
         """``p16``: fp16 tensor to receive a copy of the updated parameters (the hash table's
         gather shadow), or None.  ``ranges``: [(offset, n)] of the trainable elements when only
         part of the buffer trains (the rest -- frozen by partial_grad / partial_training -- gets
         no update, no weight decay and keeps its moments, as torch AdamW skips a parameter whose
         grad is None); None: the whole buffer.  ``before(i)`` runs before range i is issued (the
         chunked table reduction waits there for chunk i's all-reduce); one step either way, the
-        update is element-wise, so a split into ranges changes no result."""
+        update is element-wise, so a split into ranges changes no result.  ``zero_grad``: the kernel
+        leaves ``grad`` all zero (storing 0 only where it was not), so a sparse scatter can add
+        into it next step without a dense fill (ABI 17; the stage-a table gradient)."""
         self.step_count += 1
         p = self.flat.detach()
         for i, (off, n) in enumerate([(0, p.numel())] if ranges is None else ranges):
@@ -133,7 +135,7 @@ class FusedAdamW:
             L.call("mli_adamw", L.AdamwArgs(L.ptr(p[off:]), L.ptr(grad[off:]), L.ptr(self.m[off:]),
                                             L.ptr(self.v[off:]), n, float(lr), self.betas[0], self.betas[1],
                                             self.eps, self.wd, self.step_count,
-                                            L.ptr(None if p16 is None else p16[off:])))
+                                            L.ptr(None if p16 is None else p16[off:]), 1 if zero_grad else 0))
 
     def resize(self, numel):
         """Moments for a parameter whose size changed (a table-size rule switch on load)."""
@@ -157,13 +159,62 @@ def reduce_gradients(grad, world_size, group=None):
     return grad
 
 
+def grad_class_ranges(items):
+    """{dW class: [(offset, length)]} of the stage-b flat gradient (engine.GRAD_CLASSES: the
+    output layers, the hidden layers, layer 0 of each head), adjacent parameters merged.
+    ``items``: Model._trainable_items()."""
+    from .engine import GRAD_CLASS_LAYERS
+    cls_of = {li: c for c, lis in GRAD_CLASS_LAYERS.items() for li in lis}
+    out = {c: [] for c in GRAD_CLASS_LAYERS}
+    for name, _, off, n in items:
+        parts = name.split(".")
+        c = cls_of[int(parts[parts.index("linears") + 1])]
+        r = out[c]
+        if r and r[-1][0] + r[-1][1] == off:
+            r[-1] = (r[-1][0], r[-1][1] + n)
+        else:
+            r.append((off, n))
+    return out
+
+
+class OverlappedGradReduce:
+    """DDP-style overlap of the stage-b gradient average with the backward (DDP's buckets,
+    imaginaire/trainers/utils/get_trainer.py:81-88, static_graph=True config_base.yaml:58-60):
+    as each dW class of the backward completes its layers' gradient (RenderEngine.backward
+    ``on_class``), that class's ranges of the flat buffer go out as async all-reduces (RCCL on
+    its own stream, behind the compute stream's work so far) while the next class's dW runs;
+    ``finish`` adds the metric slots, waits once and divides by the world size.  Every element
+    sees the serial form's operations (its rank sum, / world); a two-rank sum is exact in any
+    order, so at world size 2 the result is bit-identical to reduce_gradients (tested)."""
+
+    def __init__(self, grad_full, ranges, world_size, group=None):
+        self.grad, self.ranges, self.world, self.group = grad_full, ranges, world_size, group
+        self.works = []
+
+    def __call__(self, cls):
+        import torch.distributed as dist
+        for o, k in self.ranges[cls]:
+            self.works.append(dist.all_reduce(self.grad[o:o + k], op=dist.ReduceOp.SUM, group=self.group,
+                                              async_op=True))
+
+    def finish(self, tail_off):
+        import torch.distributed as dist
+        self.works.append(dist.all_reduce(self.grad[tail_off:], op=dist.ReduceOp.SUM, group=self.group,
+                                          async_op=True))
+        for w in self.works:
+            w.wait()   # NCCL: the compute stream waits; gloo: the host does
+        self.works = []
+        self.grad.div_(self.world)
+        return self.grad
+
+
 def table_chunks(n, chunk):
     """[(offset, length)] cutting n elements into pieces of ``chunk`` (the last one ragged)."""
     chunk = max(1, int(chunk))
     return [(o, min(chunk, n - o)) for o in range(0, n, chunk)]
 
 
-def reduce_and_step_table(optim, grad, lr, p16, world_size, chunk, overlap=True, group=None):
+def reduce_and_step_table(optim, grad, lr, p16, world_size, chunk, overlap=True, group=None, zero_grad=False):
     """Stage a: average the hash-table gradient over the ranks (DDP wraps the table with every
     other parameter, imaginaire/trainers/utils/get_trainer.py:80-88) and take the table's AdamW
     step.  At 2^22 entries per level the gradient is 1.46 GB, so the serial form -- ONE all-reduce,
@@ -176,12 +227,12 @@ def reduce_and_step_table(optim, grad, lr, p16, world_size, chunk, overlap=True,
     ``overlap=False`` (the deterministic mode) keeps the single collective for more ranks, whose
     ring order depends on the message split."""
     if world_size == 1:
-        optim.step(grad, lr, p16=p16)
+        optim.step(grad, lr, p16=p16, zero_grad=zero_grad)
         return
     import torch.distributed as dist
     if not overlap:
         reduce_gradients(grad, world_size, group)
-        optim.step(grad, lr, p16=p16)
+        optim.step(grad, lr, p16=p16, zero_grad=zero_grad)
         return
     chunks = table_chunks(grad.numel(), chunk)
     works = [dist.all_reduce(grad[o:o + k], op=dist.ReduceOp.SUM, group=group, async_op=True) for o, k in chunks]
@@ -190,7 +241,7 @@ def reduce_and_step_table(optim, grad, lr, p16, world_size, chunk, overlap=True,
         works[i].wait()   # NCCL: the current stream waits for chunk i; gloo: the host does
         o, k = chunks[i]
         grad[o:o + k].div_(world_size)
-    optim.step(grad, lr, p16=p16, ranges=chunks, before=ready)
+    optim.step(grad, lr, p16=p16, ranges=chunks, before=ready, zero_grad=zero_grad)
 
 
 class ZeroTableAdamW:
@@ -400,12 +451,10 @@ class Trainer:
             self.optim = FusedAdamW(model.flat, lr=o.params.lr, weight_decay=o.params.weight_decay)
             if self.stage == "a":
                 # stage a trains the hash table too (one AdamW group, NeuralLumen/model.py:422-438);
-                # over several ranks its optimizer state is sharded (ZeroTableAdamW) unless the
-                # deterministic mode keeps the single all-reduce (cfg.trainer.zero_table: False
-                # forces the replicated form)
-                zero = cfg.trainer.get("zero_table", None)
-                if zero is None:
-                    zero = world_size > 1 and not model.deterministic
+                # over several ranks cfg.trainer.zero_table: True shards its optimizer state
+                # (ZeroTableAdamW).  Opt-in: the sharded form is gloo-tested only, no
+                # multi-GPU RCCL run has checked it against the replicated default on hardware
+                zero = bool(cfg.trainer.get("zero_table", False)) and not model.deterministic
                 if zero and world_size > 1:
                     import torch.distributed as dist
                     self.optim_table = ZeroTableAdamW(model.neural_sdf.tcnn_encoding.params, world_size,
@@ -420,6 +469,13 @@ class Trainer:
             if model.neural_sdf.c2f is not None:   # neuralangelo/trainer.py:30-32
                 model.neural_sdf.warm_up_end = o.sched.warm_up_end
         self._grad_table = None
+        # stage a: the table AdamW leaves the consumed table gradient zero for the next scatter
+        # (mli_adamw zero_grad: only the touched entries rewritten, no 1.46 GB fill per step);
+        # False keeps the averaged gradient readable after the step (tests)
+        self.table_grad_consume = True
+        # stage b over several ranks: the gradient all-reduce per dW class, overlapped with the
+        # next class's dW (OverlappedGradReduce); False: one collective after the backward
+        self.grad_overlap = None
         # stage a over several ranks: the table gradient's all-reduce in chunks, each chunk's
         # AdamW issued behind its own reduction (reduce_and_step_table); 2^25 elements = 128 MiB.
         # None: overlapped unless the deterministic mode is on; True / False force it
@@ -548,9 +604,11 @@ class Trainer:
             self._stepped = set()
         return self._stepped
 
-    def _step_table(self, grad, lr):
+    def _step_table(self, grad, lr, consume=False):
         """The table's averaged-gradient AdamW step: sharded (ZeroTableAdamW) or replicated
-        (reduce_and_step_table: one all-reduce, or chunks overlapped with their AdamW)."""
+        (reduce_and_step_table: one all-reduce, or chunks overlapped with their AdamW).
+        ``consume`` (the fused step's own gradient buffer, replicated form): the AdamW leaves the
+        buffer zeroed for the next hash-grid scatter (RenderEngine.backward_a then skips its fill)."""
         eng = self.model.engine
         if isinstance(self.optim_table, ZeroTableAdamW):
             z = self.optim_table
@@ -561,9 +619,14 @@ class Trainer:
                 pad[:grad.numel()].copy_(grad.reshape(-1))
             z.step(pad, lr)
             self._table_synced = False
+            self.model.table_sharded_stale = True
+            self._shadow_current()
             return
+        consume = consume and not self.model.deterministic
         reduce_and_step_table(self.optim_table, grad, lr, eng.table16, self.world_size, self.table_chunk,
-                              overlap=self._table_overlap())
+                              overlap=self._table_overlap(), zero_grad=consume)
+        if consume:
+            eng.table_grad_clean = grad.data_ptr()
 
     def sync_table(self):
         """ZeRO table: gather the fp32 master and the moments (a collective: every rank calls it,
@@ -572,6 +635,17 @@ class Trainer:
         if isinstance(self.optim_table, ZeroTableAdamW) and not getattr(self, "_table_synced", True):
             self._table_full_moments = self.optim_table.sync()
             self._table_synced = True
+            self.model.table_sharded_stale = False
+            self._shadow_current()
+
+    def _shadow_current(self):
+        """ZeRO table: the all-gathered fp16 shadow is the table the kernels read; mark it current
+        for the table's present version, so that Model.prepare does not re-cast it from the fp32
+        master (stale outside this rank's shard between syncs, and equal to it after one)."""
+        m = self.model
+        if m.engine is not None and m._sdf_version is not None:
+            t = m.neural_sdf.tcnn_encoding.params
+            m._sdf_version = (t._version, t.data_ptr())
 
     def _table_overlap(self):
         return (not self.model.deterministic) if self.table_overlap is None else bool(self.table_overlap)
@@ -726,6 +800,16 @@ class Trainer:
             self._grad = torch.empty(n + N_METRICS, device=m.flat.device)
         return self._grad[:n], self._grad[n:]
 
+    def _grad_reducer(self, m):
+        """Several ranks: the per-class overlapped all-reduce (``grad_overlap`` None / True), or
+        None for the single collective after the backward (``grad_overlap`` False, one rank)."""
+        if self.world_size <= 1 or self.grad_overlap is False:
+            return None
+        key = (id(self._grad), self._grad.numel())
+        if getattr(self, "_class_ranges_key", None) != key:
+            self._class_ranges_key, self._class_ranges = key, grad_class_ranges(m._trainable_items())
+        return OverlappedGradReduce(self._grad, self._class_ranges, self.world_size)
+
     def _publish(self, lv):
         """Step losses / PSNR as tensors of their own (the buffer tail is rewritten next step)."""
         lv = lv.clone()
@@ -754,6 +838,7 @@ class Trainer:
             self._gate_ev.record()
         eng.gate_wgrad = self.prefetch_gate == "wgrad"
         grad, lv = self._grad_buffer()  # every element is written by the backward / the loss kernel
+        red = self._grad_reducer(m)
         if fused:
             # composite + losses + composite backward in one launch (mli_composite_loss)
             rays, dists, fld, hd, _ = st
@@ -763,18 +848,23 @@ class Trainer:
                                            self._loss_args(rays, fld, None, data, lv), defer=True)
             st = (rays, dists, fld, hd, comp)
             try:
-                eng.backward(st, None, None, None, None, m.flat, m._sdf_l1(), grad, dz4=dz4)
+                eng.backward(st, None, None, None, None, m.flat, m._sdf_l1(), grad, dz4=dz4,
+                             **({} if red is None else {"on_class": red}))
             except BaseException:
                 eng.drop_deferred()
                 raise
             eng.finish_losses()
         else:
             d_rgb, d_o_r, d_o_s, d_o_re = self._fused_losses(st, data, lv)
-            eng.backward(st, d_rgb, d_o_r, d_o_s, d_o_re, m.flat, m._sdf_l1(), grad)
+            eng.backward(st, d_rgb, d_o_r, d_o_s, d_o_re, m.flat, m._sdf_l1(), grad,
+                         **({} if red is None else {"on_class": red}))
         m._last_state = st
         if eng.gate_wgrad:
             self._gate_ev, eng.gate_event = eng.gate_event, None
-        reduce_gradients(self._grad, self.world_size)   # gradients + metrics, one collective
+        if red is None:
+            reduce_gradients(self._grad, self.world_size)   # gradients + metrics, one collective
+        else:
+            red.finish(grad.numel())   # the metric slots (loss values: after finish_losses), wait, / world
         m.set_flat_grad(grad)
         self._step_flat(grad, self.lr())
         self.current_iteration += 1
@@ -854,7 +944,7 @@ class Trainer:
         self._step_flat(grad, lr)
         if self.table_trains():
             # (a frozen table needs no averaged gradient: no collective for it)
-            self._step_table(self._grad_table, lr)
+            self._step_table(self._grad_table, lr, consume=self.table_grad_consume)
         self.current_iteration += 1
         self._publish(lv)
         return m.outputs(st) if return_outputs else None
@@ -908,7 +998,11 @@ class Trainer:
                 out.append((name, p, self.optim.m[off:off + k].view(shape), self.optim.v[off:off + k].view(shape)))
             elif self.optim_table is not None and p is self.model.neural_sdf.tcnn_encoding.params:
                 if isinstance(self.optim_table, ZeroTableAdamW):
-                    # the full moments exist only as sync_table() gathered them (None: never stepped)
+                    # the full moments exist only as sync_table() gathered them (None: never stepped);
+                    # after a later step they are stale: refuse rather than return them
+                    if not getattr(self, "_table_synced", True):
+                        raise RuntimeError("the ZeRO-sharded table moments are not gathered since the last "
+                                           "step: call trainer.sync_table() on every rank first")
                     mv = self._table_full_moments
                     out.append((name, p, None if mv is None else mv[0], None if mv is None else mv[1]))
                 else:
@@ -984,6 +1078,7 @@ class Trainer:
                         z.m.zero_()
                         z.v.zero_()
                     self._table_full_moments, self._table_synced = None, True
+                    self.model.table_sharded_stale = False
                     continue
                 if not st:
                     m.zero_()

@@ -318,13 +318,16 @@ def neus_alphas(s_var, ray_unit, sdfs, grads, dists, far, progress, anneal_end):
 
 
 def render_rays(weights, cfg, center, ray_unit, pts_light, u=None, training=True, progress=0.0,
-                dists=None, geometry=None):
+                dists=None, geometry=None, geometry_st=None):
     """NeuralLumen/model.py:232-336 render_rays_lumen + :338-403 render_rays_object_lumen,
     network_mode 'rgb_r_s', no background NeRF, no light visibility.  ``dists`` (test hook)
     replaces the hierarchical sampler's output, to condition downstream comparisons;
     ``geometry`` (test hook, with ``dists``) replaces the SDF network's outputs at those samples
     -- dict(sdfs [B,R,N,1] (outside already overwritten), grads [B,R,N,3], feats [B,R,N,256],
-    hess or None) -- so that only the heads, the compositing and the losses are the oracle's."""
+    hess or None) -- so that only the heads, the compositing and the losses are the oracle's.
+    ``geometry_st`` (test hook, same keys): the forward VALUES of the SDF network's outputs are
+    the given ones, the backward runs through the oracle's own graph (straight-through,
+    v + (given - v).detach()): the stage-a gradients conditioned on another forward's geometry."""
     with torch.no_grad():
         if cfg.bounding == "box":
             near, far, outside = aabb_bounds(center, ray_unit, cfg.aabb)
@@ -337,6 +340,12 @@ def render_rays(weights, cfg, center, ray_unit, pts_light, u=None, training=True
         sdfs, feats = sdf_net(weights, cfg, pts, with_feat=True)
         sdfs = torch.where(outside[..., None].expand_as(sdfs), torch.full_like(sdfs, cfg.outside_val), sdfs)
         grads, hess = sdf_taps(weights, cfg, pts, sdfs, training)
+        if geometry_st is not None:
+            st = lambda v, g: v + (g.to(v.dtype) - v).detach()   # noqa: E731
+            sdfs, grads, feats = st(sdfs, geometry_st["sdfs"]), st(grads, geometry_st["grads"]), \
+                st(feats, geometry_st["feats"])
+            if hess is not None and geometry_st.get("hess") is not None:
+                hess = st(hess, geometry_st["hess"])
     else:
         sdfs, grads, feats, hess = geometry["sdfs"], geometry["grads"], geometry["feats"], geometry.get("hess")
     normals = F.normalize(grads, dim=-1)
@@ -424,7 +433,7 @@ def light_visibility(weights, cfg, vis, center, ray_unit, pts_light, near, far, 
 
 
 def forward(weights, cfg, data, u=None, training=True, progress=0.0, width=512, height=None, dists=None,
-            geometry=None):
+            geometry=None, geometry_st=None):
     """NeuralLumen/model.py:113-131 Model.forward -> render_pixels_lumen."""
     height = height or width
     center, ray = pixel_rays(data["pose"], data["intr"], data["ray_idx"], width, height)
@@ -432,7 +441,8 @@ def forward(weights, cfg, data, u=None, training=True, progress=0.0, width=512, 
     pts_light = light_points(data["pose_light"], height * width)
     bidx = torch.arange(ray.shape[0])[:, None].expand_as(data["ray_idx"])
     pts_light = pts_light[bidx, data["ray_idx"]]
-    out = render_rays(weights, cfg, center, ray_unit, pts_light, u, training, progress, dists, geometry)
+    out = render_rays(weights, cfg, center, ray_unit, pts_light, u, training, progress, dists, geometry,
+                      geometry_st)
     vis = getattr(cfg, "light_visibility", None)
     if vis and not training:  # NeuralLumen/model.py:325-336 (flag_light_visibility)
         if cfg.bounding == "box":

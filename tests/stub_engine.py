@@ -73,10 +73,17 @@ class StubEngine:
         fld = dict(grad=torch.zeros(N, R, 3), hess=torch.zeros(N, R, 3))
         return rays, torch.zeros(N, R), fld, {}, comp
 
-    def backward(self, st, d_rgb, d_o_r, d_o_s, d_o_re, flat, sdf_l1, grad_out):
+    def backward(self, st, d_rgb, d_o_r, d_o_s, d_o_re, flat, sdf_l1, grad_out, dz4=None, on_class=None):
         x = st[0]["x"]
         grad_out.zero_()
         grad_out[:3] = (d_rgb * x[:, None]).sum(0)
+        # every element rank-specific, so that each class range's reduction is exercised
+        k = torch.arange(3, grad_out.numel(), dtype=torch.float64)
+        grad_out[3:] = (torch.sin(k * 1e-3) * float(x.double().sum()) + torch.cos(k * 7e-4) * float(
+            (d_rgb.double() * x.double()[:, None]).sum())).float()
+        if on_class is not None:   # RenderEngine.backward's per-class completion, in launch order
+            for c in ("out", "big", "wide"):
+                on_class(c)
         return grad_out
 
     def load_table(self, params_flat):
@@ -109,9 +116,9 @@ def stub_losses(trainer, st, data, lv):
     return d_rgb, z, z[:, :1], z
 
 
-def stub_adamw_step(self, grad, lr, p16=None, ranges=None, before=None):
+def stub_adamw_step(self, grad, lr, p16=None, ranges=None, before=None, zero_grad=False):
     """torch.optim.AdamW's update on the flat buffer (FusedAdamW.step's semantics, incl. ranges,
-    the per-range hook and the fp16 copy)."""
+    the per-range hook, the fp16 copy and the consumed gradient left zero)."""
     self.step_count += 1
     b1, b2 = self.betas
     for i, (off, n) in enumerate([(0, self.flat.numel())] if ranges is None else ranges):
@@ -126,6 +133,8 @@ def stub_adamw_step(self, grad, lr, p16=None, ranges=None, before=None):
         p.addcdiv_(m, denom, value=-lr / (1 - b1 ** self.step_count))
         if p16 is not None:
             p16[off:off + n].copy_(p)
+        if zero_grad:
+            g.zero_()
 
 
 def install(monkeypatch=None):

@@ -208,7 +208,7 @@ def _step_result_a(tr, m):
                 total=float(tr.losses["total"]), world=tr.world_size)
 
 
-def _run_a(frame, world, overlap=True, chunk=1 << 14, steps=2, monkeypatch=None, install=True):
+def _run_a(frame, world, overlap=True, chunk=1 << 14, steps=2, monkeypatch=None, install=True, consume=False):
     from mli_nerf_amd import synthetic
     from mli_nerf_amd.trainer import Trainer
     stub, cfg, m = _stub_setup_a()
@@ -217,6 +217,7 @@ def _run_a(frame, world, overlap=True, chunk=1 << 14, steps=2, monkeypatch=None,
     cfg.trainer.zero_table = False   # the replicated table path (ZeRO: test_stage_a_zero_table_matches_replicated)
     tr = Trainer(cfg, is_inference=False, model=m, world_size=world)
     tr.table_overlap, tr.table_chunk = overlap, chunk
+    tr.table_grad_consume = consume   # False: the averaged table gradient stays readable (gtab)
     tr.current_iteration = 100000   # past the coarse-to-fine ramp
     grads = []
     for s in range(steps):
@@ -232,6 +233,7 @@ def _train_a_worker(rank, port, results):
     try:
         results[(rank, "overlap")] = _run_a(rank, WORLD, overlap=True)
         results[(rank, "serial")] = _run_a(rank, WORLD, overlap=False, install=False)
+        results[(rank, "consume")] = _run_a(rank, WORLD, overlap=True, install=False, consume=True)
     finally:
         dist.destroy_process_group()
 
@@ -264,9 +266,13 @@ def test_stage_a_step_world2_stub_engine(monkeypatch):
         for s in range(2):
             a, b = results[(r, "overlap")][s], results[(0, "overlap")][s]
             c = results[(r, "serial")][s]
+            z = results[(r, "consume")][s]
             for k in ("table", "table16", "m_tab", "v_tab", "flat", "gtab"):
                 assert torch.equal(a[k], b[k]), (r, s, k)   # replicas in sync
                 assert torch.equal(a[k], c[k]), (r, s, k)   # overlapped == serial, bitwise
+                if k != "gtab":   # the consumed gradient: left zero for the next scatter (ABI 17)
+                    assert torch.equal(a[k], z[k]), (r, s, k)
+            assert not bool(z["gtab"].any())
             assert torch.equal(a["table16"], a["table"].half())
 
 
@@ -429,3 +435,137 @@ def test_bench_launcher_world2(tmp_path, capfd):
     line = json.loads(out[-1])
     assert line == {"n_gpus": WORLD, "sum": 3.0, "argv": ["--steps", "3"]}
     assert bench.launch_workers(WORLD, ["--fail"], script=str(w)) == 3
+
+
+def _zero_guard_worker(rank, world, port, results):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mli_nerf_amd import synthetic
+        from mli_nerf_amd.trainer import Trainer, ZeroTableAdamW
+        stub, cfg, m = _stub_setup_a()
+        stub.install(None)
+        cfg.trainer["zero_table"] = True
+        tr = Trainer(cfg, is_inference=False, model=m, world_size=world)
+        assert isinstance(tr.optim_table, ZeroTableAdamW)
+        tr.table_overlap = False
+        tr.current_iteration = 100000
+        got = {}
+        tr.train_step(synthetic.make_batch(32, frame=rank))
+        tr.sync_table()
+        tr.optim_state_dict()            # gathered: fine
+        tr.train_step(synthetic.make_batch(32, frame=rank + 10))
+        tr.train_step(synthetic.make_batch(32, frame=rank + 20))   # two steps without a sync
+        for what, fn in (("optim_state_dict", tr.optim_state_dict),
+                         ("save_checkpoint", lambda: tr.save_checkpoint("/nonexistent-not-written")),
+                         ("prepare", lambda: (setattr(m, "engine", None), setattr(m, "_sdf_version", None),
+                                              m.prepare()))):
+            try:
+                fn()
+                got[what] = "no error"
+            except RuntimeError as e:
+                got[what] = "sync_table" in str(e)
+        stub.install(None)   # (the prepare probe dropped the engine)
+        tr.sync_table()      # collective: every rank
+        tr.optim_state_dict()
+        m.prepare()
+        got["after_sync"] = True
+        results[rank] = got
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_zero_table_stale_state_guards():
+    """with the table ZeRO-sharded, the fp32 master outside this rank's shard and the
+    gathered moments are only valid right after sync_table().  Two steps without a sync must make
+    optim_state_dict, save_checkpoint and an engine rebuild (Model.prepare re-casting the fp16
+    shadow from the fp32 master) raise instead of returning stale state or reverting the other
+    ranks' updates; after sync_table() all three work again."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    results = ctx.Manager().dict()
+    mp.start_processes(_zero_guard_worker, args=(2, port, results), nprocs=2, join=True, start_method="spawn")
+    for r in range(2):
+        assert results[r] == {"optim_state_dict": True, "save_checkpoint": True, "prepare": True,
+                              "after_sync": True}, results[r]
+
+
+def _overlap_worker(rank, port, results):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        from mli_nerf_amd import synthetic
+        from mli_nerf_amd.trainer import Trainer
+        for overlap in (True, False):
+            stub, cfg, m = _stub_setup()
+            stub.install()
+            tr = Trainer(cfg, is_inference=False, model=m)
+            tr.grad_overlap = overlap
+            tr.current_iteration = 10000
+            calls = []
+            if overlap:
+                real = tr._grad_reducer
+
+                def spy(model, real=real):
+                    red = real(model)
+                    orig = red.__call__
+
+                    class Spy:
+                        def __call__(self, cls):
+                            calls.append(cls)
+                            orig(cls)
+
+                        def finish(self, off):
+                            calls.append("finish")
+                            return red.finish(off)
+                    return Spy()
+                tr._grad_reducer = spy
+            for s in range(2):
+                tr.train_step(synthetic.make_batch(32, frame=rank + 10 * s))
+            res = _step_result(tr, m)
+            res["calls"] = calls
+            results[(rank, overlap)] = res
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_trainer_grad_allreduce_overlap_world2():
+    """the stage-b gradient average issued per dW class as each class's layers
+    complete (DDP-bucket style, overlapped with the next class's dW) is bit-identical to the single
+    all-reduce after the backward, on 2 ranks with different rays over two steps: gradient, every
+    parameter after the AdamW step, and the averaged loss / PSNR metrics; the classes go out in the
+    backward's launch order, then the metric slots."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    results = ctx.Manager().dict()
+    mp.start_processes(_overlap_worker, args=(port, results), nprocs=WORLD, join=True, start_method="spawn")
+    for r in range(WORLD):
+        a, b = results[(r, True)], results[(r, False)]
+        assert a["calls"] == ["out", "big", "wide", "finish"] * 2, a["calls"]
+        assert torch.equal(a["grad"], b["grad"])
+        assert torch.equal(a["flat"], b["flat"])
+        assert torch.equal(a["flat"], results[(0, True)]["flat"])
+        for k in ("psnr", "total", "render"):
+            assert a[k] == b[k], k
+    assert not torch.equal(results[(0, True)]["grad"], torch.zeros_like(results[(0, True)]["grad"]))
+
+
+def test_grad_class_ranges_cover_the_flat_buffer():
+    """The per-class ranges of OverlappedGradReduce tile the stage-b flat gradient exactly once."""
+    from mli_nerf_amd.configs import preset
+    from mli_nerf_amd.model import Model
+    from mli_nerf_amd.trainer import grad_class_ranges
+    cfg = preset("syn_hotdog_b", rays=32, n_coarse=16, n_fine=4, log2T=12)
+    m = Model(cfg.model, cfg.data)
+    rng = grad_class_ranges(m._trainable_items())
+    assert sorted(rng) == ["big", "out", "wide"]
+    cover = torch.zeros(m.flat.numel(), dtype=torch.int32)
+    for c, lst in rng.items():
+        for o, k in lst:
+            cover[o:o + k] += 1
+    assert bool((cover == 1).all())
+    assert len(rng["out"]) == 3 and len(rng["big"]) == 3 and len(rng["wide"]) == 3

@@ -245,3 +245,62 @@ def test_stage_a_world2_on_one_gpu_overlap_equals_serial():
             if k != "gtab":   # (the sharded path's gradient buffer holds this rank's own sum)
                 assert torch.equal(results[(r, "zero")][k], results[(r, "serial")][k]), (r, k)
     assert not torch.equal(results[(0, "overlap")]["table"], _two_steps_a(1)["table"])   # the ranks averaged
+
+
+def test_consumed_gradients_left_zero():
+    """ABI 17: the fused stage-a step issues no fill for its accumulators.  The table AdamW leaves
+    the table gradient it consumed all zero (mli_adamw zero_grad stores 0 only where the entry was
+    not), and the weight-norm assemble leaves the split-K dW buffer zero (zero_dw): after a step
+    both are exactly zero, so the next step's scatter / atomics add into clean buffers.  The next
+    step's table gradient then equals one accumulated into a freshly zeroed buffer (support
+    identical; values to fp32 atomic-order noise)."""
+    _need_gpu()
+    cfg, model, trainer, sd, data, u = _setup(64, 16, 4, 100000)
+    batch = {k: v.to(DEV) for k, v in data.items()}
+    trainer.train_step(batch, u=u.to(DEV))
+    torch.cuda.synchronize()
+    eng = model.engine
+    assert eng.table_grad_clean == trainer._grad_table.data_ptr()
+    assert not bool(trainer._grad_table.any())
+    assert not bool(eng._bufs["dw_a"].any())
+    b2 = {k: v.to(DEV) for k, v in synthetic.make_batch(64, frame=11).items()}
+    trainer.compute_grads_a(b2, u=u.to(DEV))            # into the buffer the AdamW cleaned
+    g_clean = trainer._grad_table.clone()
+    eng.table_grad_clean = None                         # force the dense fill
+    trainer.compute_grads_a(b2, u=u.to(DEV))
+    torch.cuda.synchronize()
+    g_fill = trainer._grad_table
+    assert torch.equal(g_clean != 0, g_fill != 0)
+    assert _cos(g_clean.cpu(), g_fill.cpu()) > 0.9999999
+    check("consumed table grad rel", float((g_clean - g_fill).norm() / g_fill.norm()), 1e-6, "<=")
+
+
+def test_stage_b_dw_left_zero():
+    """Stage b: every dW / db element the weight-norm assemble reads is left zero by it (no fill
+    in the next step).  (The packed layer-0 columns a head has no input for -- mlp_r's SH rows --
+    are never read; WIDE writes them through its slab sum, so their content is never used.)"""
+    _need_gpu()
+    import numpy as np
+    from mli_nerf_amd import layout
+    from mli_nerf_amd.model import Model
+    from mli_nerf_amd.trainer import Trainer
+    cfg = preset("syn_hotdog_b", rays=512, n_coarse=32, n_fine=8, log2T=14)
+    m = Model(cfg.model, cfg.data)
+    m.load_state_dict(synthetic.make_state_dict(log2T=14))
+    tr = Trainer(cfg, is_inference=False, model=m.to(DEV))
+    tr.current_iteration = 10000
+    for f in range(2):
+        tr.train_step({k: v.to(DEV) for k, v in synthetic.make_batch(512, frame=f).items()})
+        torch.cuda.synchronize()
+        eng = m.engine
+        dw = eng._bufs["dw"].cpu()
+        assert eng._dw_zero == eng._bufs["dw"].data_ptr()
+        off = 0
+        for hdx, (name, k_in, k_out) in enumerate(layout.HEADS):
+            for li in range(5):
+                mm, kk = eng._dw_sizes()[hdx * 5 + li]
+                w, b = dw[off:off + mm * kk].view(mm, kk), dw[off + mm * kk:off + mm * kk + mm]
+                off += mm * kk + mm
+                cols = torch.from_numpy(layout.head_kinv(name, k_in).astype(np.int64)) if li == 0 else slice(None)
+                assert not bool(w[:, cols].any()) and not bool(b.any()), (name, li)
+        assert torch.isfinite(m.flat.grad).all() and float(m.flat.grad.abs().sum()) > 0

@@ -1,0 +1,308 @@
+"""Where the stage-a gradient error comes from, as test_gpu_grad_decomp.py
+splits the stage-b one.
+
+``test_gpu_stage_a.test_stage_a_gradients_match_oracle`` compares the GPU's stage-a parameter
+gradients with the fp32 CPU oracle fed only the GPU's sampled depths and the fp16-rounded table:
+per tensor cosine >= 0.995 and relative error <= 10 % (measured up to 4 %).  Two legs split it.
+
+(b) fp16 emulation.  Every kernel of the stage-a backward is re-run in float64 from the GPU's OWN
+    operands -- the stored fragment images (layout.unfrag), the weights rounded to fp16 as the
+    pack kernels round them, the fp32 vectors the previous kernel wrote -- and compared with
+    what that kernel made of them:
+      * the head (mli_rgb_fwd, mli_geo_bwd's dX chain): X_{l+1} = relu(W_l X_l + b_l) and
+        dZ_l = mask_l (W_{l+1}^T dZ_{l+1}), each from the GPU's own input image;
+      * mli_geo_bwd's geometry tail: d normal = (W0^T dZ0)[normal rows] (fp32),
+        dZ1sdf = (W0^T dZ0)[feat rows] * (1 - exp(-100 feat)), d h0 = W1sdf^T dZ1sdf;
+      * mli_sdf_bwd: d sdf of the 5 points from the eikonal / curvature / normalize / stencil
+        formulas on the GPU's d_sdf, d_grad, d_nrm, gradients and hessians; layer 0 recomputed
+        from the FIELD's encoding image; dZ0 = (w_sdf ds + [center] d h0) * sigmoid(100 z0);
+        d enc = W0_enc^T dZ0; linear_sdf's dW / db = sum ds softplus(z0) / sum ds;
+      * mli_hash_bwd: the table gradient as the trilinear scatter of the GPU's d enc over the 5
+        points' corners (oracle/hashgrid.py's cells, indices and weights), in float64;
+      * mli_wgrad + mli_grad_assemble: every parameter's gradient (the 5S-sample SDF layer-0 dW
+        over [enc, p] included) from the GPU's dZ / X images, through the weight-norm backward.
+    Bars: fp16-rounded outputs <= 2e-3 relative, fp32 outputs <= 1e-4, every parameter gradient
+    <= 0.2 % relative, the table gradient cosine >= 0.99999 with identical support.  A kernel
+    defect shows up here, not as percent-level drift against the fp32 oracle.
+(a) The fp32 oracle conditioned on the GPU's geometry: its SDF network's values at the samples
+    (sdf, gradients, hessians, the SDF feature) are replaced by the GPU's in the forward
+    (straight-through: v_o + (v_gpu - v_o).detach()), the backward runs through the oracle's own
+    fp32 graph.  What remains is the backward's fp16 gradient images and operands against fp32:
+    <= 2 % per tensor.  The unconditioned comparison keeps its 10 % bar
+    (test_gpu_stage_a.py): the rest of its error is the forward's fp16 SDF amplified through the
+    4-tap normals into the head's inputs.
+
+Every bar goes through ``margins.check`` (recorded with MLI_MARGINS_OUT)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from margins import check
+from mli_nerf_amd import layout, synthetic
+from mli_nerf_amd.configs import preset
+from oracle import hashgrid as o_hash
+from oracle import render as o_render
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+# (R, Nc, Nf, iteration): iteration 20000 -> 8 active levels; 80000 -> 15 active levels
+CASES = [(64, 16, 4, 20000), (32, 64, 16, 80000)]
+
+
+def _rel(a, b):
+    a, b = torch.as_tensor(a).double(), torch.as_tensor(b).double()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+def _cos(a, b):
+    a, b = a.double().flatten(), b.double().flatten()
+    return float((a @ b) / (a.norm() * b.norm()).clamp_min(1e-300))
+
+
+def _wn(sd, pre):
+    v, g = sd[pre + ".weight_v"].double(), sd[pre + ".weight_g"].double()
+    return g * v / v.norm(dim=1, keepdim=True)
+
+
+def _wn16(sd, pre):
+    """The weight-normed weight as the pack kernels hand it to the MFMAs: rounded to fp16."""
+    return _wn(sd, pre).float().half().double()
+
+
+def _wn_backward(sd, pre, dw, db):
+    """torch.nn.utils.weight_norm backward (dim 0) in float64: grads of weight_v, weight_g, bias."""
+    v, g = sd[pre + ".weight_v"].double(), sd[pre + ".weight_g"].double()
+    nrm = v.norm(dim=1, keepdim=True)
+    vh = v / nrm
+    gg = (dw * vh).sum(1, keepdim=True)
+    gv = (g / nrm) * (dw - gg * vh)
+    return gv, gg, db
+
+
+def _tile_order(x, N, R):
+    """[N][R](...) sample-major (slot k R + r) -> tile order m = r N + k, features first."""
+    x = x.reshape(N, R, -1).permute(1, 0, 2).reshape(N * R, -1)
+    return x.t()
+
+
+def _setup(R, Nc, Nf, it, log2T=14, s_var=3.0):
+    from mli_nerf_amd.model import Model
+    from mli_nerf_amd.trainer import Trainer
+    cfg = preset("syn_hotdog_a", rays=R, n_coarse=Nc, n_fine=Nf, log2T=log2T)
+    model = Model(cfg.model, cfg.data)
+    sd = synthetic.make_state_dict(log2T=log2T, s_var=s_var, heads="rgb")
+    model.load_state_dict(sd)
+    model = model.to(DEV)
+    trainer = Trainer(cfg, is_inference=False, model=model)
+    trainer.current_iteration = it
+    trainer._start_of_iteration()
+    data = synthetic.make_batch(R, frame=3)
+    u = synthetic.stratified_uniforms(R, Nc, seed=5)
+    return cfg, model, trainer, sd, data, u
+
+
+@pytest.mark.parametrize("R,Nc,Nf,it", CASES)
+def test_stage_a_gradient_error_decomposition(R, Nc, Nf, it):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    cfg, model, trainer, sd, data, u = _setup(R, Nc, Nf, it)
+    trainer.table_grad_consume = False
+    st, lv = trainer.compute_grads_a({k: v.to(DEV) for k, v in data.items()}, u=u.to(DEV))
+    torch.cuda.synchronize()
+    eng = model.engine
+    rays, dists, fld, hd, comp = st
+    N = dists.shape[0]
+    S = N * R
+    scale = float(2.0 ** round(math.log2(max(R, 1)) + 2))   # RenderEngine.backward_a's loss scale
+    g_flat = trainer._grad[:model.flat.numel()].double().cpu()
+    offs = {name: (off, shape) for name, shape, off in model._layout_items()}
+    cpu = lambda t: t.detach().double().cpu()   # noqa: E731
+
+    def gpu_grad(name):
+        off, shape = offs[name]
+        return g_flat[off:off + max(1, int(np.prod(shape)))].reshape(shape)
+
+    B = eng._bufs
+    worst = {}
+
+    def chk(key, name, val, bar, op="<="):
+        worst[key] = max(worst.get(key, 0.0), val) if op == "<=" else min(worst.get(key, 1.0), val)
+        check(name, val, bar, op)
+
+    # ------------------------------------------------------------ leg (b): the head
+    head = layout.HEADS_A[0][0]
+    kmap = torch.from_numpy(layout.head_kmap(head).astype(np.int64))
+    kinv = torch.from_numpy(layout.head_kinv(head, 294).astype(np.int64))
+    W = [_wn16(sd, layout.param_prefix(head, li)) for li in range(5)]
+    bias = [sd[layout.param_prefix(head, li) + ".bias"].double() for li in range(5)]
+    w0p = torch.zeros(256, layout.K0, dtype=torch.float64)
+    w0p[:, kmap >= 0] = W[0][:, kmap[kmap >= 0]]
+    x0 = cpu(layout.unfrag(hd["x0T"], layout.K0))                                  # [304][S]
+    X = [x0] + [cpu(layout.unfrag(hd["xT"][0, j], 256)) for j in range(4)]         # inputs of linears 0..4
+    Wl = [w0p] + W[1:]
+    for j in range(4):
+        emu = torch.relu(Wl[j] @ X[j] + bias[j][:, None]).float().half().double()
+        chk("fp16 out", "stage-a head fwd X%d rel" % (j + 1), _rel(X[j + 1], emu), 2e-3)
+    dzT = B["dzT"][:4 * 256 * S].view(4, 256 * S)
+    dZ = [cpu(layout.unfrag(dzT[li], 256)) for li in range(4)]
+    dz4 = cpu(layout.unfrag(B["dz4T"][:16 * S], 16, kst=1))[:3]                     # fp16 rows 0..2
+    above = [dz4, dZ[3], dZ[2], dZ[1]]
+    for step, li in enumerate((3, 2, 1, 0)):
+        emu = (W[li + 1].t() @ above[step] * (X[li + 1] > 0)).float().half().double()
+        chk("fp16 out", "stage-a head bwd dZ%d rel" % li, _rel(dZ[li], emu), 2e-3)
+    # geometry tail of mli_geo_bwd
+    dX0 = w0p.t() @ dZ[0]                                                           # [304][S], scaled
+    d_nrm = _tile_order(cpu(B["d_nrm"][:S * 4]), N, R)[:3]
+    chk("fp32 out", "stage-a d_nrm rel", _rel(d_nrm, dX0[259:262]), 1e-4)
+    feat = x0[:256]
+    dz1 = cpu(layout.unfrag(B["dz1T"][:256 * S], 256))
+    emu = (dX0[:256] * (1.0 - torch.exp(-100.0 * feat))).float().half().double()
+    chk("fp16 out", "stage-a dZ1sdf rel", _rel(dz1, emu), 2e-3)
+    w1s = _wn16(sd, "neural_sdf.mlp.linears.1")
+    dh0 = cpu(layout.unfrag(B["dh0"][:S * 256], 256))
+    emu = (w1s.t() @ dz1).float().half().double()
+    chk("fp16 out", "stage-a d h0 rel", _rel(dh0, emu), 2e-3)
+
+    # ------------------------------------------------------------ leg (b): mli_sdf_bwd
+    # the 5 points per sample exactly as field_points (fp32: p = c + v d, taps p + k eps)
+    to_t = lambda t, c: _tile_order(t.detach().cpu(), N, R).t().reshape(S, c)    # noqa: E731  [S][c] tile order
+    d_t = to_t(dists, 1)[:, 0]
+    r_of = torch.arange(S) // N
+    c0 = rays["center"].detach().cpu().reshape(R, 3)[r_of]
+    v0 = rays["ray_unit"].detach().cpu().reshape(R, 3)[r_of]
+    p0 = c0 + v0 * d_t[:, None]                                                     # fp32, two roundings
+    e = float(eng.eps)
+    ks = torch.tensor([[0, 0, 0], [1, -1, -1], [-1, -1, 1], [-1, 1, -1], [1, 1, 1]], dtype=torch.float32)
+    pts = [p0 if i == 0 else p0 + ks[i] * e for i in range(5)]                        # [5] x [S][3] fp32
+    out_r = rays["outside"].detach().cpu().reshape(R)[r_of].bool()
+    g = to_t(fld["grad"], 3).double()
+    hs = to_t(fld["hess"], 3).double()
+    dsdf = to_t(B["d_sdf"][:S], 1)[:, 0].double()
+    dg = to_t(B["d_grad"][:3 * S], 3).double()
+    nrm_d = to_t(B["d_nrm"][:4 * S], 4)[:, :3].double() / scale
+    w_eik, w_curv = trainer.weights.get("eikonal", 0.0), trainer.weights.get("curvature", 0.0)
+    gn = g.norm(dim=1)
+    f_eik = torch.where(~out_r & (gn > 0), w_eik / S * 2.0 * (gn - 1.0) / gn.clamp_min(1e-300), torch.zeros_like(gn))
+    dg = dg + f_eik[:, None] * g
+    dot = (nrm_d * g).sum(1)
+    big = gn > 1e-12
+    dg = dg + torch.where(big[:, None], nrm_d / gn.clamp_min(1e-300)[:, None]
+                          - g * (dot / gn.clamp_min(1e-300) ** 3)[:, None], nrm_d * 1e12)
+    lap = hs.sum(1)
+    dH = torch.where(~out_r & (lap != 0), w_curv / S * torch.sign(lap), torch.zeros_like(lap))
+    gd, hh = 1.0 / eng.grad_den, 0.5 * dH / eng.hess_den
+    ds = torch.stack([torch.where(out_r, torch.zeros_like(dsdf), dsdf - 2.0 * dH / eng.hess_den),
+                      (dg[:, 0] - dg[:, 1] - dg[:, 2]) * gd + hh, (-dg[:, 0] - dg[:, 1] + dg[:, 2]) * gd + hh,
+                      (-dg[:, 0] + dg[:, 1] - dg[:, 2]) * gd + hh, (dg[:, 0] + dg[:, 1] + dg[:, 2]) * gd + hh]) * scale
+    # layer 0 at the 5 points from the FIELD's encoding image (tile 5 t + p of the 5S images)
+    enc5 = cpu(layout.unfrag(fld["enc"], 128, kst=8, order="nat"))                 # [128][5S]
+    dz0_5 = cpu(layout.unfrag(B["dz0_frag"][:5 * S * 256], 256))                   # [256][5S]
+    denc5 = layout.unfrag(B["d_enc"][:S * 640], 128, kst=8, order="nat").double().cpu()
+    p16_5 = cpu(layout.unfrag(B["p_frag"][:5 * S * 16], 16, kst=1, order="nat"))[:3]
+    col = lambda p: (torch.arange(S) // 32 * 5 + p) * 32 + torch.arange(S) % 32   # noqa: E731
+    w0 = _wn(sd, "neural_sdf.mlp.linears.0")
+    w0e16 = w0[:, 3:].float().half().double()
+    b0 = sd["neural_sdf.mlp.linears.0.bias"].double()
+    w_sdf = sd["neural_sdf.mlp.linear_sdf.weight"].double().reshape(256)
+    dW_sdf = torch.zeros(256, dtype=torch.float64)
+    for p in range(5):
+        cp = col(p)
+        z0 = w0e16 @ enc5[:, cp] + w0[:, :3] @ pts[p].double().t() + b0[:, None]
+        dh = w_sdf[:, None] * ds[p][None] + (dh0 if p == 0 else 0.0)
+        emu = (dh * torch.sigmoid(100.0 * z0)).float().half().double()
+        chk("fp16 out", "stage-a dZ0 point %d rel" % p, _rel(dz0_5[:, cp], emu), 2e-3)
+        emu = w0e16.t() @ dz0_5[:, cp] / scale
+        chk("fp32 out", "stage-a d enc point %d rel" % p, _rel(denc5[:, cp], emu), 1e-4)
+        chk("fp16 out", "stage-a p16 point %d rel" % p, _rel(p16_5[:, cp], pts[p].t().half().double()), 0.0)
+        sp = F.softplus(z0, beta=100)
+        dW_sdf += (sp * ds[p][None]).sum(1) / scale
+    chk("grad", "stage-a emulated grad rel linear_sdf.weight",
+        _rel(gpu_grad("neural_sdf.mlp.linear_sdf.weight").reshape(256), dW_sdf), 2e-3)
+    chk("grad", "stage-a emulated grad rel linear_sdf.bias",
+        _rel(gpu_grad("neural_sdf.mlp.linear_sdf.bias").reshape(1), ds.sum().reshape(1) / scale), 2e-3)
+
+    # ------------------------------------------------------------ leg (b): mli_hash_bwd
+    sdf_m = model.neural_sdf
+    table, _ = o_hash.level_table(log2T=14)
+    act = int(sdf_m.active_levels)
+    n_par = model.neural_sdf.tcnn_encoding.params.numel()
+    grid = torch.zeros(n_par // 8, 8, dtype=torch.float64)
+    dummy = torch.zeros(n_par)
+    for p in range(5):
+        x01 = (pts[p] + 2.0) * 0.25
+        _, cache = o_hash._encode_fwd(x01, dummy, table[:act], 8)
+        dp = denc5[:, col(p)].t()                                                    # [S][128]
+        for lvl, (rows, ws) in enumerate(cache):
+            gl = dp[:, lvl * 8:(lvl + 1) * 8]
+            for c in range(8):
+                grid.index_add_(0, rows[:, c], ws[c].double()[:, None] * gl)
+    gt = trainer._grad_table.double().cpu()
+    emu = grid.reshape(-1)
+    chk("table", "stage-a emulated table grad cos", _cos(gt, emu), 0.99999, ">=")
+    chk("grad", "stage-a emulated table grad rel", _rel(gt, emu), 2e-3)
+    check("stage-a emulated table grad support mismatch", float(((gt != 0) ^ (emu != 0)).sum()), 0, "<=")
+
+    # ------------------------------------------------------------ leg (b): mli_wgrad + assemble
+    ops = [(dZ[0], x0), (dZ[1], X[1]), (dZ[2], X[2]), (dZ[3], X[3]), (dz4, X[4])]
+    for li, (a, b) in enumerate(ops):
+        pre = layout.param_prefix(head, li)
+        dw, db = (a @ b.t()) / scale, a.sum(1) / scale
+        if li == 0:
+            dw = dw[:, kinv]
+        for suffix, ref in zip((".weight_v", ".weight_g", ".bias"), _wn_backward(sd, pre, dw, db)):
+            chk("grad", "stage-a emulated grad rel " + pre + suffix,
+                _rel(gpu_grad(pre + suffix), ref.reshape(gpu_grad(pre + suffix).shape)), 2e-3)
+    h0 = cpu(layout.unfrag(fld["h0"], 256))
+    pre = "neural_sdf.mlp.linears.1"
+    for suffix, ref in zip((".weight_v", ".weight_g", ".bias"),
+                           _wn_backward(sd, pre, dz1 @ h0.t() / scale, dz1.sum(1) / scale)):
+        chk("grad", "stage-a emulated grad rel " + pre + suffix,
+            _rel(gpu_grad(pre + suffix), ref.reshape(gpu_grad(pre + suffix).shape)), 2e-3)
+    bmat = torch.cat([p16_5, enc5], 0)                                              # reference columns 0..130
+    pre = "neural_sdf.mlp.linears.0"
+    for suffix, ref in zip((".weight_v", ".weight_g", ".bias"),
+                           _wn_backward(sd, pre, dz0_5 @ bmat.t() / scale, dz0_5.sum(1) / scale)):
+        chk("grad", "stage-a emulated grad rel " + pre + suffix,
+            _rel(gpu_grad(pre + suffix), ref.reshape(gpu_grad(pre + suffix).shape)), 2e-3)
+    print("leg (b) worst:", {k: "%.2e" % v for k, v in worst.items()})
+    # diagnostic for leg (a): the share of the backward's fp16 image elements in fp16's subnormal
+    # range (|x| < 2^-14), where the relative precision falls below fp16's 2^-11
+    sub = lambda t: float(((t != 0) & (t.abs() < 2.0 ** -14)).double().mean())   # noqa: E731
+    print("fp16 subnormal share: dZ0..3 %s dz1sdf %.3f dZ0sdf %.3f feat %.3f" % (
+        ["%.3f" % sub(z) for z in dZ], sub(dz1), sub(dz0_5), sub(feat)))
+
+    # ------------------------------------------------------------ leg (a): conditioned oracle
+    pcfg = o_render.PathCfg(n_coarse=Nc, n_fine=Nf, log2T=14, rgb_mode="rgb", active_levels=act,
+                            anneal_levels=int(sdf_m.anneal_levels))
+    sd16 = dict(sd)
+    sd16["neural_sdf.tcnn_encoding.params"] = sd["neural_sdf.tcnn_encoding.params"].half().float()
+    sd_o = {k: v.clone().requires_grad_(True) for k, v in sd16.items()}
+    to_rn = lambda t, c: t.detach().cpu().reshape(N, R, c).permute(1, 0, 2)[None].float()   # noqa: E731
+    geometry_st = dict(sdfs=to_rn(fld["sdf"], 1), grads=to_rn(fld["grad"], 3), hess=to_rn(fld["hess"], 3),
+                       feats=x0[:256].float().t().reshape(R, N, 256)[None])
+    o_out = o_render.forward(sd_o, pcfg, data, u=u, training=True, progress=model.progress,
+                             dists=model.outputs(st)["dists"].detach().cpu(), geometry_st=geometry_st)
+    total, losses, _ = o_render.stage_a_losses(o_out, data, trainer.weights["curvature"])
+    total.backward()
+    lvc = lv.cpu()
+    for i, k in enumerate(("render", "eikonal", "curvature")):
+        check("conditioned loss %s rel" % k, abs(lvc[i].item() - losses[k].item()) / (abs(losses[k].item()) + 1e-4),
+              1e-3, "<=")
+    worst_a = 0.0
+    for name, shape, off in model._layout_items():
+        gg, o = gpu_grad(name).float(), sd_o[name].grad
+        if name == "s_var":
+            rel = abs(gg.item() - o.item()) / max(abs(o.item()), 1e-12)
+        else:
+            rel = _rel(gg, o)
+            check("conditioned grad cos " + name, _cos(gg, o), 0.999, ">=")
+        worst_a = max(worst_a, rel)
+        check("conditioned grad rel " + name, rel, 0.02, "<=")
+    ot = sd_o["neural_sdf.tcnn_encoding.params"].grad
+    check("conditioned table grad cos", _cos(trainer._grad_table.cpu(), ot), 0.999, ">=")
+    print("leg (a) worst rel %.4f" % worst_a)
+    assert math.isfinite(worst_a)

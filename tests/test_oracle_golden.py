@@ -129,3 +129,44 @@ def test_oracle_light_visibility_matches_reference_golden(golden, name):
             assert torch.equal(got, ref), key
         else:
             torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5, msg=key)
+
+
+def test_oracle_straight_through_geometry_hook(golden):
+    """The conditioning hook of the stage-a decomposition (tests/test_gpu_stage_a_decomp.py leg
+    (a)): given the oracle's own SDF-network values as ``geometry_st``, the forward outputs and
+    every parameter gradient equal the unhooked oracle's; given shifted values, the outputs move
+    with them while the gradients still flow into the SDF network and the hash table."""
+    fx = golden(STAGE_A_CASES[0])
+    cfg = case_cfg({**fx, "config": "syn_hotdog_b"})
+    cfg.rgb_mode, cfg.active_levels, cfg.anneal_levels = "rgb", fx["active_levels"], fx["anneal_levels"]
+    data = synthetic.make_batch(fx["R"], H=fx["H_img"], W=fx["W_img"], frame=3)
+    runs = []
+    for hook in (None, "self", "shift"):
+        sd = synthetic.make_state_dict(log2T=fx["log2T"], seed=0, s_var=fx["s_var"], heads="rgb")
+        sd = {k: v.requires_grad_(True) for k, v in sd.items()}
+        kw = dict(u=fx["u"], training=True, progress=fx["progress"], width=fx["W_img"], height=fx["H_img"])
+        geo = None
+        if hook is not None:
+            with torch.no_grad():
+                ref = runs[0][0]
+                d = 1e-3 if hook == "shift" else 0.0
+                geo = dict(sdfs=ref["sdfs"] + d, grads=ref["gradients"] * (1 + d), hess=ref["hessians"],
+                           feats=runs[0][2])
+        out = o_render.forward(sd, cfg, data, dists=None if hook is None else runs[0][0]["dists"],
+                               geometry_st=geo, **kw)
+        total, _, _ = o_render.stage_a_losses(out, data, fx["curvature_weight"])
+        total.backward()
+        feats = None
+        if hook is None:   # the SDF feature at the samples, recomputed for the hook
+            with torch.no_grad():
+                center, ray = o_render.pixel_rays(data["pose"], data["intr"], data["ray_idx"], fx["W_img"], fx["H_img"])
+                p = center[..., None, :] + torch.nn.functional.normalize(ray, dim=-1)[..., None, :] * out["dists"]
+                feats = o_render.sdf_net({k: v.detach() for k, v in sd.items()}, cfg, p, with_feat=True)[1]
+        runs.append((out, {k: v.grad.clone() for k, v in sd.items() if v.grad is not None}, feats))
+    (o0, g0, _), (o1, g1, _), (o2, g2, _) = runs
+    torch.testing.assert_close(o1["rgb"], o0["rgb"], rtol=0, atol=1e-6)
+    for k in g0:
+        torch.testing.assert_close(g1[k], g0[k], rtol=1e-5, atol=1e-9)
+    assert not torch.allclose(o2["rgb"], o0["rgb"], rtol=0, atol=1e-7)
+    assert float(g2["neural_sdf.tcnn_encoding.params"].abs().sum()) > 0
+    assert float(g2["neural_sdf.mlp.linears.0.weight_v"].abs().sum()) > 0

@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--rays", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--membw", action="store_true", help="also time plain HBM write / copy streams")
+    ap.add_argument("--ray-order", default="random", choices=["random", "sorted", "xcd"],
+                    help="order of the batch's rays: as drawn, sorted by pixel, or sorted and dealt to "
+                         "the 8 XCDs by image band (workgroup b runs on XCD b %% 8)")
     args = ap.parse_args()
     if args.membw:
         x = torch.empty(2 * 1024 ** 3, dtype=torch.float16, device="cuda")  # 4 GiB
@@ -54,6 +57,16 @@ def main():
     model = model.to(dev)
     tr = Trainer(cfg, is_inference=False, model=model)
     batch = {k: v.to(dev) for k, v in synthetic.make_batch(args.rays, frame=0).items()}
+    if args.ray_order != "random":
+        idx = batch["ray_idx"].reshape(-1)
+        order = torch.argsort(idx)
+        if args.ray_order == "xcd":   # band x of the sorted rays -> slots x, x + 8, x + 16, ...
+            n = order.numel()
+            order = order.reshape(8, n // 8).t().reshape(-1)
+        for k, v in list(batch.items()):
+            if v.dim() >= 2 and v.shape[1] == idx.numel():
+                batch[k] = v[:, order]
+        print("ray order", args.ray_order)
     for _ in range(3):
         tr.train_step(batch)
     torch.cuda.synchronize()
