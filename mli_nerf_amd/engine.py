@@ -765,7 +765,7 @@ class RenderEngine:
         rays, dists, fld, hd, comp = st
         N, R = dists.shape
         S = N * R
-        scale = float(2.0 ** round(math.log2(max(R, 1)) + 2))
+        scale = self.grad_scale(R)   # (x8 / x64 measured: leg (a) of test_gpu_stage_a_decomp unchanged)
         f16 = torch.float16
         dz4, d_sdf, d_grad = self._buf("dz4", (N, R, 8)), self._buf("d_sdf", (N, R)), self._buf("d_grad", (N, R, 3))
         dinv = self._buf("d_inv_s_part", (R,))

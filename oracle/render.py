@@ -138,6 +138,43 @@ def aabb_bounds(center, ray_unit, aabb):
 # --------------------------------------------------------------------------------------
 # neural SDF (projects/neuralangelo/utils/{modules,mlp}.py)
 # --------------------------------------------------------------------------------------
+# matmul operand precision: None = fp32, "tf32" = the reference's own GEMM arithmetic
+# (imaginaire/trainers/base.py:172-178 sets torch.backends.cuda.matmul.allow_tf32): operands
+# rounded to TF32's 10-bit mantissa, fp32 accumulate, in the forward and in both backward GEMMs.
+MATMUL_OPERANDS = None
+
+
+def tf32_round(x):
+    """Round fp32 to TF32 (10-bit mantissa, fp32 exponent), nearest-even, as a value."""
+    i = x.detach().contiguous().view(torch.int32)
+    r = (i + 0x0FFF + ((i >> 13) & 1)) & ~0x1FFF
+    return r.view(torch.float32)
+
+
+class _Tf32Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        x2 = tf32_round(x.reshape(-1, x.shape[-1]))
+        y = x2 @ tf32_round(w).t() + b
+        return y.reshape(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        g2 = tf32_round(gy.reshape(-1, gy.shape[-1]))
+        x2 = tf32_round(x.reshape(-1, x.shape[-1]))
+        gx = (g2 @ tf32_round(w)).reshape(x.shape)
+        return gx, g2.t() @ x2, gy.reshape(-1, gy.shape[-1]).sum(0)
+
+
+def linear(x, w, b):
+    """F.linear at the oracle's matmul precision (MATMUL_OPERANDS)."""
+    if MATMUL_OPERANDS == "tf32":
+        return _Tf32Linear.apply(x, w, b)
+    return F.linear(x, w, b)
+
+
 def wn(weights, prefix):
     """torch weight_norm(dim=0): W = g * v / ||v||_row (nerf_util.py:177-178, mlp.py:42-43)."""
     v, g = weights[prefix + ".weight_v"], weights[prefix + ".weight_g"]
@@ -164,13 +201,13 @@ def sdf_net(weights, cfg, pts, with_feat):
         mask[..., :cfg.active_levels * 8] = 1
         enc = enc * mask
     inp = torch.cat([flat, enc], dim=-1)
-    h0 = softplus100(F.linear(inp, wn(weights, "neural_sdf.mlp.linears.0"),
+    h0 = softplus100(linear(inp, wn(weights, "neural_sdf.mlp.linears.0"),
                               weights["neural_sdf.mlp.linears.0.bias"]))
-    sdf = F.linear(h0, weights["neural_sdf.mlp.linear_sdf.weight"],
+    sdf = linear(h0, weights["neural_sdf.mlp.linear_sdf.weight"],
                    weights["neural_sdf.mlp.linear_sdf.bias"])
     feat = None
     if with_feat:
-        feat = softplus100(F.linear(h0, wn(weights, "neural_sdf.mlp.linears.1"),
+        feat = softplus100(linear(h0, wn(weights, "neural_sdf.mlp.linears.1"),
                                     weights["neural_sdf.mlp.linears.1.bias"]))
         feat = feat.reshape(*shape, -1)
     return sdf.reshape(*shape, 1), feat
@@ -278,7 +315,7 @@ def head_mlp(weights, name, x):
     h = x
     for li in range(5):
         pre = "neural_rgb.%s.linears.%d" % (name, li)
-        h = F.linear(h, wn(weights, pre), weights[pre + ".bias"])
+        h = linear(h, wn(weights, pre), weights[pre + ".bias"])
         if li < 4:
             h = F.relu(h)
     return h
