@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--ray-order", default="random", choices=["random", "sorted", "xcd"],
                     help="order of the batch's rays: as drawn, sorted by pixel, or sorted and dealt to "
                          "the 8 XCDs by image band (workgroup b runs on XCD b %% 8)")
+    ap.add_argument("--dump", default=None, help="save the sampler's dists and the field's outputs (bit-identity A/B)")
     args = ap.parse_args()
     if args.membw:
         x = torch.empty(2 * 1024 ** 3, dtype=torch.float16, device="cuda")  # 4 GiB
@@ -73,6 +74,10 @@ def main():
     eng = model.engine
     rays, dists, fld, hd, comp = model._last_state
     R, N = args.rays, model.pcfg.n_samples
+    if args.dump:
+        d0 = eng.sample(rays, None)
+        f0 = eng.field(rays, d0, True)
+        torch.save({"dists": d0.cpu(), **{k: f0[k].cpu() for k in ("sdf", "grad", "hess", "h0") if k in f0}}, args.dump)
     res = {}
     res["sample (all rounds)"] = timeit(lambda: eng.sample(rays, None), args.reps)
     res["sdf field"] = timeit(lambda: eng.field(rays, dists, True), args.reps)
