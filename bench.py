@@ -78,7 +78,7 @@ def kernel_flops(name, R, N, Nc, Nf, H, stage="b"):
     return 0
 
 
-PMC_SUMMARY = os.environ.get("MLI_PMC_SUMMARY") or os.path.join(HERE, "profiles", "r5", "final", "pmc_summary.json")
+PMC_SUMMARY = os.environ.get("MLI_PMC_SUMMARY") or os.path.join(HERE, "profiles", "r6", "final", "pmc_summary.json")
 PMC_SAMPLES = 4096 * 128  # the workload the committed PMC passes ran (tools/pmc.sh: bench.py defaults)
 
 
