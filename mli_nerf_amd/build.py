@@ -14,7 +14,12 @@ SOURCES = ["rays.hip", "sdf.hip", "mlp_fwd.hip", "mlp_fwd_pq.hip", "mlp_fwd_trai
            "wgrad.hip", "params.hip", "loss.hip"]
 # sdf.hip: no SLP packing, so fma(fp16 -> fp32 feature, w, acc) selects v_fma_mix_f32 (one
 # instruction) instead of v_cvt_f32_f16 x2 + v_pk_fma_f32
-PER_FILE = {"sdf.hip": ["-fno-slp-vectorize"]}
+# No SLP packing of scalar fp32 math in the MFMA and geometry kernels: v_pk_*_f32 beside MFMAs
+# costs more than the two scalar ops it replaces (MI355X_MICROARCH.md, 'price of one filler') and
+# its even-aligned register pairs raise the VGPR count (field_mlp 167 -> 118).
+# rays.hip / params.hip (VALU-only sampling, AdamW) keep it.
+PER_FILE = {s: ["-fno-slp-vectorize"] for s in ("sdf.hip", "mlp_fwd.hip", "mlp_fwd_pq.hip", "mlp_fwd_train.hip",
+                                                 "mlp_bwd.hip", "mlp_geo.hip", "wgrad.hip", "loss.hip")}
 FLAGS = ["-O3", "--offload-arch=gfx950", "-fPIC", "-std=c++17", "-ffp-contract=off",
          "-I", os.path.join(REPO, "include"), "-I", CSRC]
 # the device assembly of every file stays next to its object (-save-temps=obj), so that build()

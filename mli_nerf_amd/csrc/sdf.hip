@@ -125,7 +125,7 @@ MLI_FI float sdf_from_enc(const uint8_t* lds, const half8 (&enc)[8], int lane, f
         const f32x2 v = softplus100x2((f32x2){acc[4 * u + j], acc[4 * u + j + 1]});
         sp[4 * u + j] = v.x;
         sp[4 * u + j + 1] = v.y;
-        part2 = __builtin_elementwise_fma((f32x2){ws[j], ws[j + 1]}, v, part2);
+        part2 = fma_x2((f32x2){ws[j], ws[j + 1]}, v, part2);
       }
     }
     if (h0_tile) {  // read by the next kernel only: non-temporal
