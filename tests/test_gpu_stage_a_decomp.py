@@ -320,9 +320,20 @@ def test_stage_a_gradient_error_decomposition(R, Nc, Nf, it):
         bar = max(0.02, 2.0 * rel_t)
         rel_gt = (abs(gg.item() - t.item()) / max(abs(t.item()), 1e-12)) if name == "s_var" else _rel(gg, t)
         print("leg (a) %-45s gpu-fp32 %.4f  tf32-fp32 %.4f  gpu-tf32 %.4f  bar %.4f" % (name, rel, rel_t, rel_gt, bar))
-        for q, v in (("tf32 oracle vs fp32 oracle rel ", rel_t), ("gpu vs tf32 oracle rel ", rel_gt)):
-            RECORDS.append({"test": _test_id(), "quantity": q + name, "measured": v, "op": "info", "bar": None,
-                            "ok": True})
+        RECORDS.append({"test": _test_id(), "quantity": "tf32 oracle vs fp32 oracle rel " + name, "measured": rel_t,
+                        "op": "info", "bar": None, "ok": True})
+        # Against the reference's own arithmetic the GPU is tight wherever it computes in that
+        # precision class (fp16 = TF32's 10-bit mantissa): every tensor but SDF layer 0 and the sdf
+        # head, whose GPU path keeps the point coordinates and the sdf dot in fp32
+        # and so sits nearer the fp32 oracle than TF32 does.
+        if name.startswith(("neural_sdf.mlp.linears.0.", "neural_sdf.mlp.linear_sdf.")):
+            RECORDS.append({"test": _test_id(), "quantity": "gpu vs tf32 oracle rel " + name, "measured": rel_gt,
+                            "op": "info", "bar": None, "ok": True})
+        else:
+            try:
+                check("gpu vs tf32 oracle rel " + name, rel_gt, 2e-3, "<=")
+            except AssertionError as e:
+                fails.append(str(e))
         try:
             check("conditioned grad rel " + name, rel, bar, "<=", note="bar = max(2 %%, 2 x tf32 %.4f)" % rel_t)
         except AssertionError as e:
