@@ -795,10 +795,20 @@ __global__ __launch_bounds__(256) void sdf_bwd_reduce_kernel(mli_sdf_bwd_args a,
 // fp32 atomic per corner feature); a tap in another cell scatters its own 64.  (A level-major
 // variant, one level per launch so the atomic working set is Infinity-Cache sized, measured
 // slower in round 1: 17.8 vs 15.7 ms before the coalesced scatter.)
+#ifndef MLI_HB_VROW
+#define MLI_HB_VROW 68
+#endif
+#ifndef MLI_HB_SROW
+#define MLI_HB_SROW 9
+#endif
 __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
-  // per wave: up to 64 run totals (64 floats) + their 8 corner slots, for the coalesced scatter
-  __shared__ __attribute__((aligned(16))) float s_vals[4][64 * 64];
-  __shared__ uint32_t s_slot[4][64 * 8];
+  // per wave: up to 64 run totals (64 floats) + their 8 corner slots, for the coalesced scatter.
+  // Rows padded (VROW = 68 floats, SROW = 9 slots) so that the tail lanes' row writes fall in
+  // distinct banks: at 64 / 8 the rows of consecutive ranks shared banks (SQ_LDS_BANK_CONFLICT
+  // 50 M cycles per launch, profiles/r6/trio_a)
+  constexpr int VROW = MLI_HB_VROW, SROW = MLI_HB_SROW;
+  __shared__ __attribute__((aligned(16))) float s_vals[4][64 * VROW];
+  __shared__ uint32_t s_slot[4][64 * SROW];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float* tvals = s_vals[wave];
   uint32_t* tslot = s_slot[wave];
@@ -911,12 +921,12 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
       const int rank = __popcll(tb & ((1ull << lane) - 1ull));
       const int ntail = __popcll(tb);
       if (tail) {
-        f32x4* vd = reinterpret_cast<f32x4*>(tvals + rank * 64);
+        f32x4* vd = reinterpret_cast<f32x4*>(tvals + rank * VROW);
 #pragma unroll
         for (int cc = 0; cc < 8; ++cc) {
           vd[2 * cc] = f32x4{V[cc][0], V[cc][1], V[cc][2], V[cc][3]};
           vd[2 * cc + 1] = f32x4{V[cc][4], V[cc][5], V[cc][6], V[cc][7]};
-          tslot[rank * 8 + cc] =
+          tslot[rank * SROW + cc] =
               P.offset + index_of(cellk[0] + (cc & 1), cellk[1] + ((cc >> 1) & 1), cellk[2] + ((cc >> 2) & 1));
         }
       }
@@ -931,8 +941,8 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int i = min(i0 + u, 63);
-          v[u] = tvals[i * 64 + lane];
-          slot[u] = tslot[i * 8 + (lane >> 3)];
+          v[u] = tvals[i * VROW + lane];
+          slot[u] = tslot[i * SROW + (lane >> 3)];
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {

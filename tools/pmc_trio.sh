@@ -6,7 +6,7 @@ set -o pipefail
 OUT=${1:-gpurun_out/pmc_trio}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS="--no-cpu --no-kernel-timing --steps 3 --warmup 2 --pipeline off"
+ARGS="--no-cpu --no-kernel-timing --steps 3 --warmup 2 --pipeline off ${TRIO_ARGS:-}"
 timeout -s KILL 60 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || echo "counter list failed rc=$?"
 have() { grep -qw "$1" "$OUT/counters.txt"; }
 P2=""
