@@ -798,6 +798,23 @@ __global__ __launch_bounds__(256) void sdf_bwd_reduce_kernel(mli_sdf_bwd_args a,
 #ifndef MLI_HB_VROW
 #define MLI_HB_VROW 68
 #endif
+#ifndef MLI_HB_DPP
+#define MLI_HB_DPP 1
+#endif
+// One step of hash_bwd's segmented run scan: V += (take ? V of the DPP source lane : 0) for all
+// 64 corner-feature sums (CTRL: row_shr:n = 0x110 + n, row_bcast:15 = 0x142; rows outside RMASK
+// and out-of-row sources read 0).
+template <int CTRL, int RMASK>
+MLI_FI void hb_scan_step(float (&V)[8][8], bool take) {
+#pragma unroll
+  for (int cc = 0; cc < 8; ++cc)
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      const float o = __builtin_bit_cast(
+          float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, V[cc][f]), CTRL, RMASK, 0xF, true));
+      V[cc][f] += take ? o : 0.0f;
+    }
+}
 #ifndef MLI_HB_SROW
 #define MLI_HB_SROW 9
 #endif
@@ -901,6 +918,17 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
       int span = c0 - start;
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) span = max(span, __shfl_xor(span, o));
+#if MLI_HB_DPP
+      // the segmented scan on DPP moves (VALU) instead of ds_bpermute (LDS): row_shr 1, 2, 4, 8
+      // within each 16-lane row, then row 1 / row 3 take lane 15 / 47's run prefix (row_bcast15)
+      // if their run started in the row before -- per lane [start, c0] as the bpermute form, the
+      // cross-row terms added in another order
+      if (span >= 1) hb_scan_step<0x111, 0xF>(V, c0 - 1 >= start);
+      if (span >= 2) hb_scan_step<0x112, 0xF>(V, c0 - 2 >= start);
+      if (span >= 4) hb_scan_step<0x114, 0xF>(V, c0 - 4 >= start);
+      if (span >= 8) hb_scan_step<0x118, 0xF>(V, c0 - 8 >= start);
+      if (__any(c0 >= 16 && start <= 15)) hb_scan_step<0x142, 0xA>(V, c0 >= 16 && start <= 15);
+#else
 #pragma unroll 1
       for (int d = 1; d <= span; d <<= 1) {
         const bool take = c0 - d >= start;
@@ -912,6 +940,7 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
             V[cc][f] += take ? o : 0.0f;
           }
       }
+#endif
       const uint32_t nx = __shfl_down(key[0], 1), ny = __shfl_down(key[1], 1), nz = __shfl_down(key[2], 1);
       const bool tail = (c0 == 31 || nx != key[0] || ny != key[1] || nz != key[2]) && any;
       // Coalesced scatter: the run totals go through LDS so one atomic instruction adds one
