@@ -805,6 +805,10 @@ __global__ __launch_bounds__(256) void sdf_bwd_reduce_kernel(mli_sdf_bwd_args a,
 // 64 corner-feature sums (CTRL: row_shr:n = 0x110 + n, row_bcast:15 = 0x142; rows outside RMASK
 // and out-of-row sources read 0).
 template <int CTRL, int RMASK>
+MLI_FI uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RMASK, 0xF, true);
+}
+template <int CTRL, int RMASK>
 MLI_FI void hb_scan_step(float (&V)[8][8], bool take) {
 #pragma unroll
   for (int cc = 0; cc < 8; ++cc)
@@ -899,14 +903,31 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
       // and never lengthen the scan
       const uint32_t key[3] = {mine ? cellk[0] : 0xFFFFFFFFu, mine ? cellk[1] : (uint32_t)lane,
                                mine ? cellk[2] : 0xFFFFFFFFu};
+#if MLI_HB_DPP
+      // neighbour keys by DPP wave_shr:1 / wave_shl:1 (lane 0 / 63 read 0: c0 == 0 / 31 decide)
+      const uint32_t px = dpp_u32<0x138, 0xF>(key[0]), py = dpp_u32<0x138, 0xF>(key[1]),
+                     pz = dpp_u32<0x138, 0xF>(key[2]);
+#else
       const uint32_t px = __shfl_up(key[0], 1), py = __shfl_up(key[1], 1), pz = __shfl_up(key[2], 1);
+#endif
       const bool head = c0 == 0 || px != key[0] || py != key[1] || pz != key[2];
       int start = head ? c0 : 0;  // first lane of this lane's run: max-scan of the heads
+#if MLI_HB_DPP
+      // (max is exact: the same values as the bpermute scan) in-row row_shr steps, then rows 1 / 3
+      // take lane 15 / 47's running max (start is 0 / a head index of the same half, so a row-0
+      // value is a valid lower bound for row 1)
+      start = max(start, (int)dpp_u32<0x111, 0xF>((uint32_t)start));
+      start = max(start, (int)dpp_u32<0x112, 0xF>((uint32_t)start));
+      start = max(start, (int)dpp_u32<0x114, 0xF>((uint32_t)start));
+      start = max(start, (int)dpp_u32<0x118, 0xF>((uint32_t)start));
+      start = max(start, (int)dpp_u32<0x142, 0xA>((uint32_t)start));
+#else
 #pragma unroll
       for (int d = 1; d < 32; d <<= 1) {
         const int o = __shfl_up(start, d);
         if (c0 >= d) start = max(start, o);
       }
+#endif
       // any lane of the run contributing (runs without contributions issue nothing)
       const uint64_t bal = __ballot(mine);
       const uint32_t hb = (uint32_t)(bal >> (32 * h));
@@ -916,8 +937,20 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
       if (!__any(any)) return;
       // scan steps only up to the longest run of the wave (fine levels: mostly 1-sample runs)
       int span = c0 - start;
+#if MLI_HB_DPP
+      // the wave's longest run: in-row max, then rows 1 / 3 with lane 15 / 47 and rows 2 / 3 with
+      // lane 31 (row_bcast:31 = 0x143): lane 63 holds the maximum
+      span = max(span, (int)dpp_u32<0x111, 0xF>((uint32_t)span));
+      span = max(span, (int)dpp_u32<0x112, 0xF>((uint32_t)span));
+      span = max(span, (int)dpp_u32<0x114, 0xF>((uint32_t)span));
+      span = max(span, (int)dpp_u32<0x118, 0xF>((uint32_t)span));
+      span = max(span, (int)dpp_u32<0x142, 0xA>((uint32_t)span));
+      span = max(span, (int)dpp_u32<0x143, 0xC>((uint32_t)span));
+      span = __builtin_amdgcn_readlane(span, 63);
+#else
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) span = max(span, __shfl_xor(span, o));
+#endif
 #if MLI_HB_DPP
       // the segmented scan on DPP moves (VALU) instead of ds_bpermute (LDS): row_shr 1, 2, 4, 8
       // within each 16-lane row, then row 1 / row 3 take lane 15 / 47's run prefix (row_bcast15)
@@ -941,7 +974,12 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
           }
       }
 #endif
+#if MLI_HB_DPP
+      const uint32_t nx = dpp_u32<0x130, 0xF>(key[0]), ny = dpp_u32<0x130, 0xF>(key[1]),
+                     nz = dpp_u32<0x130, 0xF>(key[2]);
+#else
       const uint32_t nx = __shfl_down(key[0], 1), ny = __shfl_down(key[1], 1), nz = __shfl_down(key[2], 1);
+#endif
       const bool tail = (c0 == 31 || nx != key[0] || ny != key[1] || nz != key[2]) && any;
       // Coalesced scatter: the run totals go through LDS so one atomic instruction adds one
       // run's 8 corners x 8 features with 8 consecutive lanes per corner (one 32 B L2 request
