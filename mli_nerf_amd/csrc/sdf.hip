@@ -529,8 +529,43 @@ MLI_FI void load_block(uint8_t* lds, const void* src_v, int pieces) {
 
 // Sum of v[0..15] over the 32 lanes of each lane half (samples), by recursive halving: lane c
 // ends with the total of register i = (c >> 1) & 15 (lanes c, c^1 both hold it).
+#ifndef MLI_HR_DPP
+#define MLI_HR_DPP 1
+#endif
+// v from lane (lane xor M) within each 32-lane half, without LDS: quad_perm for M = 1, 2; the
+// row_shl:4 / row_shr:4 pair with bank masks for M = 4; row_ror:8 for M = 8
+template <int M>
+MLI_FI float xor_lanes(float v) {
+  const int x = __builtin_bit_cast(int, v);
+  if (M == 1) return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false));
+  if (M == 2) return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false));
+  if (M == 4) {
+    const int t = __builtin_amdgcn_update_dpp(0, x, 0x104, 0xF, 0x5, false);  // banks 0, 2 <- p + 4
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(t, x, 0x114, 0xF, 0xA, false));  // 1, 3 <- p - 4
+  }
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false));  // M = 8
+}
+
 MLI_FI float half_reduce16(const float (&v)[16], int c) {
   float p8[8], p4[4], p2[2];
+#if MLI_HR_DPP
+  // the same pairwise sums as the __shfl_xor form below (a + b == b + a exactly): the xor-16 step
+  // by v_permlane16_swap (lane p of row 0 / 1 ends with both halves' own / partner values), the
+  // rest by DPP -- no LDS instructions
+  const uint32_t b3 = (c & 8) ? ~0u : 0u, b2 = (c & 4) ? ~0u : 0u, b1 = (c & 2) ? ~0u : 0u;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(uint32_t, v[j]),
+                                                     __builtin_bit_cast(uint32_t, v[j + 8]), false, false);
+    p8[j] = __builtin_bit_cast(float, (uint32_t)sw[0]) + __builtin_bit_cast(float, (uint32_t)sw[1]);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) p4[j] = sel_mask(b3, p8[j + 4], p8[j]) + xor_lanes<8>(sel_mask(b3, p8[j], p8[j + 4]));
+#pragma unroll
+  for (int j = 0; j < 2; ++j) p2[j] = sel_mask(b2, p4[j + 2], p4[j]) + xor_lanes<4>(sel_mask(b2, p4[j], p4[j + 2]));
+  const float p1 = sel_mask(b1, p2[1], p2[0]) + xor_lanes<2>(sel_mask(b1, p2[0], p2[1]));
+  return p1 + xor_lanes<1>(p1);
+#else
   // bitwise selects (a ternary on the arrays becomes a dynamically indexed scratch load)
   const uint32_t b4 = (c & 16) ? ~0u : 0u, b3 = (c & 8) ? ~0u : 0u, b2 = (c & 4) ? ~0u : 0u,
                  b1 = (c & 2) ? ~0u : 0u;
@@ -545,6 +580,7 @@ MLI_FI float half_reduce16(const float (&v)[16], int c) {
     p2[j] = sel_mask(b2, p4[j + 2], p4[j]) + __shfl_xor(sel_mask(b2, p4[j], p4[j + 2]), 4);
   const float p1 = sel_mask(b1, p2[1], p2[0]) + __shfl_xor(sel_mask(b1, p2[0], p2[1]), 2);
   return p1 + __shfl_xor(p1, 1);
+#endif
 }
 
 MLI_FI void field_points5(const float* center, const float* ray_unit, float d, int r, float e,
