@@ -837,6 +837,9 @@ __global__ __launch_bounds__(256) void sdf_bwd_reduce_kernel(mli_sdf_bwd_args a,
 #ifndef MLI_HB_DPP
 #define MLI_HB_DPP 1
 #endif
+#ifndef MLI_HB_FMAC
+#define MLI_HB_FMAC 1
+#endif
 // One step of hash_bwd's segmented run scan: V += (take ? V of the DPP source lane : 0) for all
 // 64 corner-feature sums (CTRL: row_shr:n = 0x110 + n, row_bcast:15 = 0x142; rows outside RMASK
 // and out-of-row sources read 0).
@@ -846,13 +849,23 @@ MLI_FI uint32_t dpp_u32(uint32_t v) {
 }
 template <int CTRL, int RMASK>
 MLI_FI void hb_scan_step(float (&V)[8][8], bool take) {
+#if MLI_HB_FMAC
+  // V + take * o as one fma (exact: o * 1 + V rounds once as the add did, o * 0 + V = V for finite
+  // o): a DPP move and a v_fmac per value and step instead of a move, a select and an add (an
+  // inline v_fmac_f32_dpp form raised the kernel to 284 VGPRs)
+  const float tf = take ? 1.0f : 0.0f;
+#endif
 #pragma unroll
   for (int cc = 0; cc < 8; ++cc)
 #pragma unroll
     for (int f = 0; f < 8; ++f) {
       const float o = __builtin_bit_cast(
           float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, V[cc][f]), CTRL, RMASK, 0xF, true));
+#if MLI_HB_FMAC
+      V[cc][f] = __builtin_fmaf(o, tf, V[cc][f]);
+#else
       V[cc][f] += take ? o : 0.0f;
+#endif
     }
 }
 #ifndef MLI_HB_SROW
