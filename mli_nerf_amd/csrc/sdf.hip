@@ -1099,6 +1099,17 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
 #pragma unroll
       for (int cc = 0; cc < 8; ++cc) {
         const float w = weight(pos, cc);
+#if MLI_HB_FMAC
+        // the weight split by the branch once per corner: G += w_in d (w_in = 0 off the center's
+        // cell: G + 0 d = G), T = w_out d -- an fma and a mul per element, no selects (equal values
+        // up to the sign of zeros, which the scatter skips)
+        const float w_in = same ? w : 0.0f, w_out = same ? 0.0f : w;
+#pragma unroll
+        for (int f = 0; f < 8; ++f) {
+          G[cc][f] = fmaf(w_in, d[f], G[cc][f]);
+          T[cc][f] = w_out * d[f];
+        }
+#else
 #pragma unroll
         for (int f = 0; f < 8; ++f) {
           if (same) {
@@ -1108,6 +1119,7 @@ __global__ __launch_bounds__(256) void hash_bwd_kernel(mli_hash_bwd_args a) {
             T[cc][f] = w * d[f];
           }
         }
+#endif
       }
       // a tap outside the center's cell: reduced over the runs of its own cell
       if (__any(!same && lv_on)) run_scatter(g, T, !same && lv_on);
