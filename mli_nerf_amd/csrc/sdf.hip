@@ -63,6 +63,28 @@ MLI_FI void load_rowc(const uint8_t* lds, int arr, int t, int h, float (&v)[16])
   }
 }
 
+#ifndef MLI_PTERM_MFMA
+#define MLI_PTERM_MFMA 0
+#endif
+// b0 + W0[:, 0:3] . p of n-tile t on the (otherwise idle) fp32 MFMA pipe: two
+// v_mfma_f32_32x32x2_f32 with K = (x, y) and (z, 1), A = the tile's rows of (wx, wy) / (wz, b0)
+// read from the row-constant arrays (acc order: row r of the tile is element
+// ((r >> 3) << 2) | (r & 3) of lane half (r >> 2) & 1), B = the lane's point.  Exact fp32
+// products and fp32 sums, in the MFMA's order instead of the fma chain's (the point
+// coordinates still never go through fp16); the accumulator comes out in the 32x32 layout the
+// fp16 chain continues.
+MLI_FI f32x16 pterm_mfma(const uint8_t* lds, int t, int lane, float px, float py, float pz) {
+  const int r = lane & 31, k = lane >> 5;
+  const uint8_t* base = lds + ROWC_OFF + (t * 2 + ((r >> 2) & 1)) * 64 + ((((r >> 3) << 2) | (r & 3)) * 4);
+  const float a1 = *reinterpret_cast<const float*>(base + (1 + k) * ROWC_ARRAY);   // wx | wy
+  const float a2 = *reinterpret_cast<const float*>(base + (k ? 0 : 3) * ROWC_ARRAY);  // wz | b0
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+  acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, k ? py : px, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a2, k ? 1.0f : pz, acc, 0, 0, 0);
+}
+
 // Hash encoding of one point per lane (both lane halves see the same point; half h holds
 // level 2q+h of k-step q): the B-fragment image X0^T of layer 0, NAT order.
 MLI_FI void hash_encode(const uint16_t* __restrict__ table, const mli_grid_levels& L, int active, int lane,
@@ -102,6 +124,9 @@ MLI_FI float sdf_from_enc(const uint8_t* lds, const half8 (&enc)[8], int lane, f
     const f32x4* rc = reinterpret_cast<const f32x4*>(lds + ROWC_OFF + (t * 2 + h) * 64);
     constexpr int A4 = ROWC_ARRAY / 16;  // f32x4 per array
     f32x16 acc;
+#if MLI_PTERM_MFMA
+    acc = pterm_mfma(lds, t, lane, px, py, pz);
+#else
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const f32x4 b0 = rc[u], wx = rc[A4 + u], wy = rc[2 * A4 + u], wz = rc[3 * A4 + u];
@@ -113,6 +138,7 @@ MLI_FI float sdf_from_enc(const uint8_t* lds, const half8 (&enc)[8], int lane, f
         acc[4 * u + j + 1] = v.y;
       }
     }
+#endif
     const half8* frag = reinterpret_cast<const half8*>(lds + t * 8 * 1024) + lane;
 #pragma unroll
     for (int q = 0; q < 8; ++q) acc = mfma32(frag[q * 64], enc[q], acc);
@@ -729,6 +755,9 @@ __global__ __launch_bounds__(BWD_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_arg
         const f32x4* rc = reinterpret_cast<const f32x4*>(lt + ROWC_OFF + (t * 2 + h) * 64);
         constexpr int A4 = ROWC_ARRAY / 16;  // f32x4 per array
         f32x16 acc;
+#if MLI_PTERM_MFMA
+        acc = pterm_mfma(lt, t, lane, px, py, pz);
+#else
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const f32x4 b0 = rc[u], wx = rc[A4 + u], wy = rc[2 * A4 + u], wz = rc[3 * A4 + u];
@@ -740,6 +769,7 @@ __global__ __launch_bounds__(BWD_WAVES * 64) void sdf_bwd_kernel(mli_sdf_bwd_arg
             acc[4 * u + j + 1] = v.y;
           }
         }
+#endif
         const half8* frag = reinterpret_cast<const half8*>(lt + t * 8 * 1024) + lane;
 #pragma unroll
         for (int qq = 0; qq < 8; ++qq) acc = mfma32(frag[qq * 64], E[qq], acc);
