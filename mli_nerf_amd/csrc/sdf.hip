@@ -64,7 +64,7 @@ MLI_FI void load_rowc(const uint8_t* lds, int arr, int t, int h, float (&v)[16])
 }
 
 #ifndef MLI_PTERM_MFMA
-#define MLI_PTERM_MFMA 0
+#define MLI_PTERM_MFMA 1
 #endif
 // b0 + W0[:, 0:3] . p of n-tile t on the (otherwise idle) fp32 MFMA pipe: two
 // v_mfma_f32_32x32x2_f32 with K = (x, y) and (z, 1), A = the tile's rows of (wx, wy) / (wz, b0)
